@@ -1,0 +1,222 @@
+"""Env-steps/s of the fused HIP quadrotor step (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--task LeeLanded] [--num-envs 4096]
+    torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...
+
+A "step" is one VecTask.step of the hot path over one batch of ``num_envs`` envs
+per GPU (config B of BASELINE.json by default: 4096-env x500 hover with the Lee
+controller, fp32).  Actions come from a ring of 16 synthetic batches staged in
+HBM before timing (train_vec.py:14-18 draws random actions; the Lee tasks
+ignore them, ekf_lee_landed.py:308).  Episodic returns are accumulated in-kernel
+and, once per 16-step rollout, reduced on device and all-reduced over RCCL when
+N > 1 — the single collective of the path.  Weak scaling: every
+rank simulates ``num_envs`` envs of the global id range.
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the step kernel at the bench
+workload; ``roofline_sweep`` repeats it at large N where the state no longer
+fits the 256 MiB Infinity Cache (at 4096 envs the whole state is
+cache-resident, so an HBM fraction there means nothing).  ``cpu_baseline`` times
+the float64 numpy oracle (oracle/quad_oracle.py, "port") on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec (4096 envs) + achieved HBM GB/s vs roofline, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+RING = 16
+
+# Algorithmic bytes per env-step of quad_step_kernel<TASK>: every
+# field the kernel must read and write per env, SoA f32 / i32, obs AoS f32,
+# reset i64, timeouts u8.  Reset-only and done-only traffic is excluded.
+BYTES_PER_ENV_STEP = {
+    # reset(8) p,q,v,w(52) progress(4) land_flag(4) r | p,q,v,w(52) progress(4) land_flag(4) obs(52) rew(4) reset(8) timeouts(1) w
+    "LeeLanded": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1,
+    # + target(12 r/w) + thrust(16 r/w) + actions(16 r)
+    "Ouzelum": 8 + 52 + 4 + 4 + 12 + 16 + 16 + 52 + 4 + 4 + 12 + 16 + 52 + 4 + 8 + 1,
+    # Ouzelum + fault rotor/onset/eta (12 r)
+    "QuadFault": 8 + 52 + 4 + 4 + 12 + 16 + 16 + 12 + 52 + 4 + 4 + 12 + 16 + 52 + 4 + 8 + 1,
+    # LeeLanded + prev_v(12) ekf q,P(56) pv x,P(216) waypoint(12), each r/w
+    "EKFLeeLanded": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1 + 2 * (12 + 56 + 216 + 12),
+    # EKF + dr(12 r) + platform(8 r/w) + traj type/idx/sd (12 r, 4 w)
+    "QuadTracking": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1 + 2 * (12 + 56 + 216 + 12) + 12 + 16 + 12 + 4,
+}
+BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
+                                   + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0
+EPISODE_TRACK_BYTES = 8           # ep_ret r/w when track_episodes is on
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--task", default="LeeLanded")
+    ap.add_argument("--num-envs", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--sweep", default="1048576,4194304")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+def make_env(task, n, dev, seed, off, total):
+    from ouzelum_amd import QuadVecTask
+    return QuadVecTask(task=task, num_envs=n, sim_device=str(dev), rl_device=str(dev), seed=seed,
+                       env_id_offset=off, num_envs_total=total, track_episodes=True)
+
+
+def action_ring(n, dev, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    return (torch.rand((RING, n, 4), device=dev, generator=g) * 2 - 1).contiguous()
+
+
+def kernel_time_us(env, ring, reps=200):
+    """Average duration of one step kernel from HIP events bracketing each launch on the
+    stream the kernel runs on.  The stream is first held by a spin kernel so every
+    (event, kernel, event) triple is queued before the GPU reaches it and no host
+    launch gap lands inside a bracket."""
+    dev = env.device
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    torch.cuda.synchronize(dev)
+    try:
+        torch.cuda._sleep(int(3e7))
+    except Exception:  # noqa: BLE001
+        pass
+    for s, e in evs:
+        s.record()
+        env.rollout(ring, 1)
+        e.record()
+    torch.cuda.synchronize(dev)
+    return float(np.mean([s.elapsed_time(e) for s, e in evs])) * 1e3
+
+
+def roofline_entry(task, n, us, track=True):
+    b = BYTES_PER_ENV_STEP[task] + (EPISODE_TRACK_BYTES if track else 0)
+    achieved = b * n / (us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "num_envs": n,
+            "bytes_per_env_step": b, "kernel_us": round(us, 3)}
+
+
+def cpu_baseline(task, n, seed, budget_s):
+    from oracle import quad_oracle as Q
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=seed))
+    rs = np.random.RandomState(0)
+    acts = rs.uniform(-1, 1, (RING, n, 4))
+    t0 = time.perf_counter()
+    for k in range(3):
+        o.step(acts[k % RING])
+    per = (time.perf_counter() - t0) / 3
+    steps = int(max(5, min(2000, budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    for k in range(steps):
+        o.step(acts[k % RING])
+    el = time.perf_counter() - t0
+    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/quad_oracle.py OracleEnv float64 numpy, task={task}, {n} envs x {steps} steps "
+                      f"({el:.1f} s, 1 thread)"}
+
+
+def main():
+    args = parse()
+    from ouzelum_amd.distributed import allreduce_returns, init_from_env, shard
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    n = args.num_envs
+    off, total = shard(n, rank, world)
+    env = make_env(args.task, n, dev, args.seed, off, total)
+    ring = action_ring(n, dev, args.seed + rank)
+
+    def rollouts(steps):
+        done = 0
+        mean_ret = float("nan")
+        while done < steps:
+            k = min(RING, steps - done)
+            env.rollout(ring, k)
+            stats = env.episode_stats()
+            if world > 1:
+                dist.all_reduce(stats)
+            done += k
+        return mean_ret
+
+    rollouts(args.warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rollouts(args.steps)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    value = n * world * args.steps / el
+
+    # secondary: the same steps through the Python VecTask.step() API (one ctypes call each)
+    py_rate = None
+    if rank == 0:
+        torch.cuda.synchronize(dev)
+        k = min(args.steps, 500)
+        t0 = time.perf_counter()
+        for i in range(k):
+            env.step(ring[i % RING])
+        torch.cuda.synchronize(dev)
+        py_rate = n * k / (time.perf_counter() - t0)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    us = kernel_time_us(env, ring)
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"config B: {n}-env x500 hover, Lee position controller ({args.task}), fp32, "
+                               "dt 0.01 x 2 sub-steps",
+                   "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
+                   "parallelism": f"env-sharded dp{world} (RCCL return all-reduce per 16-step rollout)"},
+        "roofline": roofline_entry(args.task, n, us),
+        "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
+    }
+    if world == 1 and not args.no_sweep:
+        sweep = []
+        del env
+        torch.cuda.empty_cache()
+        for big in [int(x) for x in args.sweep.split(",") if x]:
+            e2 = make_env(args.task, big, dev, args.seed, 0, big)
+            r2 = action_ring(big, dev, args.seed)[:2].contiguous()
+            e2.rollout(r2, 20)
+            sweep.append(roofline_entry(args.task, big, kernel_time_us(e2, r2, reps=50)))
+            del e2, r2
+            torch.cuda.empty_cache()
+        out["roofline_sweep"] = sweep
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.task, n, args.seed, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,186 @@
+/*
+ * ouzelum.h — C ABI of the MI355X-native quadrotor step (libouzelum_hip.so).
+ *
+ * Drop-in boundary for the reference's VecTask hot path.  Plain
+ * pointers and sizes only: no torch or C++ types cross this line, so ctypes
+ * (ouzelum_amd/_lib.py), cgo, JNI or N-API can bind it.  Device buffers are
+ * owned by the caller (PyTorch tensors in the Python shim); the library only
+ * keeps their pointers.  Every call returns 0 on success or a negative
+ * OUZ_ERR_* code; ouz_last_error() gives a thread-local message.
+ * Launch functions never synchronise the stream and never allocate, so a
+ * caller may capture them into a hipGraph.
+ *
+ * Reference interface each entry point replaces (paths under isaacgymenvs/):
+ *   ouz_create / ouz_bind / ouz_init_state
+ *        VecTask.__init__ + allocate_buffers   tasks/base/vec_task.py:169-223,254-277
+ *        task __init__ (tensor views, EKF/PV objects, controller)
+ *                                              tasks/ekf_lee_landed.py:48-171, tasks/ouzelum.py:42-110
+ *   ouz_step        VecTask.step               tasks/base/vec_task.py:313-359
+ *                   = pre_physics_step + gym.simulate x controlFrequencyInv + post_physics_step
+ *                                              tasks/ekf_lee_landed.py:308-530,620-685
+ *   ouz_step_n      K consecutive VecTask.step calls over a ring of action batches
+ *                   (the train_vec.py:14-18 env-only loop)
+ *   ouz_reset_idx   VecTask.reset_idx / reset_done (lazy: marks reset_buf)
+ *                                              tasks/base/vec_task.py:369-406, ekf_lee_landed.py:271-306
+ *   ouz_lee_control Controller.__call__        controllers/controller.py:45-48 (+ position/velocity/attitude)
+ *   ouz_ekf_update  EKF.update (ang branch)    ahrs_ekf.py:1280-1337
+ *   ouz_pv_predict  PVFilter.prediction_step   PVFilter.py:25-64
+ *   ouz_pv_correct  PVFilter.correction_step   PVFilter.py:67-110
+ *   ouz_integrate   gym.simulate (PhysX)       tasks/base/vec_task.py:332-335 (build-defined integrator)
+ *   ouz_reward      compute_ingenuity_reward   tasks/ekf_lee_landed.py:692-723
+ *   ouz_philox      the counter RNG every draw of the step uses (replaces torch_rand_float /
+ *                   torch.rand: ekf_lee_landed.py:284-286, ouzelum.py:183-184, utils/POMDP.py:25,30)
+ */
+#ifndef OUZELUM_H_
+#define OUZELUM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OUZ_ABI_VERSION 1
+
+/* error codes */
+#define OUZ_OK 0
+#define OUZ_ERR_INVALID (-1)
+#define OUZ_ERR_HIP (-2)
+#define OUZ_ERR_UNBOUND (-3)
+
+/* tasks (BASELINE.json configs) */
+#define OUZ_TASK_OUZELUM 0        /* RL per-rotor thrust, random goals (tasks/ouzelum.py)        config A */
+#define OUZ_TASK_LEE_LANDED 1     /* Lee position control on true state (tasks/lee_landed.py)   config B */
+#define OUZ_TASK_EKF_LEE_LANDED 2 /* AHRS-EKF + PV-KF + Lee (tasks/ekf_lee_landed.py)                    */
+#define OUZ_TASK_TRACKING 3       /* EKF pipeline + trajectory platform + DR                    config C */
+#define OUZ_TASK_FAULT 4          /* RL thrust + single-rotor fault + obs noise                 config D */
+#define OUZ_TASK_MIXED 5          /* per-64-env curriculum of tasks 1/3/4                       config E */
+#define OUZ_NUM_TASKS 6
+
+/* POMDP modes (utils/POMDP.py:5-20); -1 = task default */
+#define OUZ_POMDP_NONE 0
+#define OUZ_POMDP_FLICKER 1
+#define OUZ_POMDP_NOISE 2
+#define OUZ_POMDP_FLICKER_NOISE 3
+
+/* Lee controller modes (controllers/controller.py:13-17) */
+#define OUZ_LEE_POSITION 0
+#define OUZ_LEE_VELOCITY 1
+#define OUZ_LEE_ATTITUDE 2
+
+/* observation / action sizes (tasks/ekf_lee_landed.py:56,61) */
+#define OUZ_NUM_OBS 13
+#define OUZ_NUM_ACT 4
+
+/* Per-env SoA float rows of the state buffer fstate[OUZ_F_COUNT][num_envs]. */
+enum {
+  OUZ_F_P = 0,          /* position (3)                    root_states[:, 0:3]  */
+  OUZ_F_Q = 3,          /* orientation xyzw (4)            root_states[:, 3:7]  */
+  OUZ_F_V = 7,          /* linear velocity, world (3)      root_states[:, 7:10] */
+  OUZ_F_W = 10,         /* angular velocity, world (3)     root_states[:, 10:13]*/
+  OUZ_F_TARGET = 13,    /* target_root_positions (3)                            */
+  OUZ_F_PREV_V = 16,    /* prev_root_linvels (3)                                */
+  OUZ_F_THRUST = 19,    /* RL rotor thrusts (4)                                 */
+  OUZ_F_EKF_Q = 23,     /* EKF estimate, wxyz (4)          Q_state              */
+  OUZ_F_EKF_P = 27,     /* EKF covariance, packed sym 4x4 (10)                  */
+  OUZ_F_PV_X = 37,      /* PV filter state [p, v, b_a] (9)                      */
+  OUZ_F_PV_P = 46,      /* PV covariance, packed sym 9x9 upper (45)             */
+  OUZ_F_WAYPOINT = 91,  /* target_waypoints (3)                                 */
+  OUZ_F_PLAT = 94,      /* landing-platform xy (2)                              */
+  OUZ_F_TRAJ_SD = 96,   /* trajectory scale * direction (1)                     */
+  OUZ_F_DR = 97,        /* DR scales: mass, inertia, thrust (3)                 */
+  OUZ_F_FAULT_ETA = 100,/* faulty-rotor efficiency (1)                          */
+  OUZ_F_EP_RET = 101,   /* running episode return (RecordEpisodeStatisticsTorch) */
+  OUZ_F_EP_SUM = 102,   /* sum of returns of episodes finished since last drain  */
+  OUZ_F_COUNT = 103
+};
+/* Per-env SoA int32 rows of istate[OUZ_I_COUNT][num_envs]. */
+enum {
+  OUZ_I_PROGRESS = 0,   /* progress_buf                                         */
+  OUZ_I_TRAJ_TYPE = 1,  /* 0 lemniscate, 1 circle, 2 square                     */
+  OUZ_I_TRAJ_IDX = 2,
+  OUZ_I_FAULT_ROTOR = 3,
+  OUZ_I_FAULT_ONSET = 4,
+  OUZ_I_LAND_FLAG = 5,  /* self.flag                                            */
+  OUZ_I_LANDINGS = 6,   /* per-env landing count (self.Landoa summed)           */
+  OUZ_I_EP_CNT = 7,     /* episodes finished since last drain                   */
+  OUZ_I_COUNT = 8
+};
+
+typedef struct ouz_config {
+  int32_t task;             /* OUZ_TASK_*                                        */
+  int32_t num_envs;         /* envs on this device                               */
+  int64_t env_id_offset;    /* global id of env 0 (rank * num_envs when sharded) */
+  int64_t num_envs_total;   /* envs over all ranks (0 -> num_envs)               */
+  uint64_t seed;
+  int32_t device;           /* HIP device ordinal                                */
+  int32_t pomdp;            /* OUZ_POMDP_* or -1 for the task default            */
+  float pomdp_prob;         /* < 0 -> task default                               */
+  float dt;                 /* sim.dt (0.01)                                     */
+  int32_t substeps;         /* sim.substeps (2)                                  */
+  int32_t convergence_time; /* EKF tasks: steps of estimator warm-up (300)       */
+  float plat_speed;         /* trajectory platform speed, m/s                    */
+  float dr_lo, dr_hi;       /* DR scale range                                    */
+  float fault_eta_hi;       /* faulty rotor efficiency ~ U(0, fault_eta_hi)      */
+  float thrust_max;         /* RL thrust clamp (2000 N, ouzelum.py:91)           */
+  float thrust_rate;        /* RL thrust action scale (2000, ouzelum.py:237)     */
+  int32_t track_episodes;   /* 1: accumulate episodic return/count in-kernel
+                               (PPO/utils.py:4-35 RecordEpisodeStatisticsTorch)  */
+} ouz_config;
+
+typedef struct ouz_buffers {
+  float* fstate;            /* [OUZ_F_COUNT][num_envs] f32                       */
+  int32_t* istate;          /* [OUZ_I_COUNT][num_envs] i32                       */
+  float* obs;               /* [num_envs][13] f32, clamped to +-5 (vec_task.py:353) */
+  float* rew;               /* [num_envs] f32                                    */
+  int64_t* reset;           /* [num_envs] i64  reset_buf                         */
+  uint8_t* timeouts;        /* [num_envs] bool time_outs                         */
+} ouz_buffers;
+
+typedef struct ouz_task_info {
+  int32_t max_episode_length;
+  float z_die;
+  float land_radius;
+  int32_t pomdp;
+  float pomdp_prob;
+  int32_t uses_actions;     /* 1 for RL-thrust tasks; Lee tasks ignore actions (ekf_lee_landed.py:308) */
+} ouz_task_info;
+
+typedef struct ouz_env ouz_env;
+
+int32_t ouz_abi_version(void);
+const char* ouz_last_error(void);
+void ouz_default_config(ouz_config* cfg);
+int ouz_task_info_get(int32_t task, ouz_task_info* out);
+
+int ouz_create(const ouz_config* cfg, ouz_env** out);
+int ouz_destroy(ouz_env* env);
+int ouz_bind(ouz_env* env, const ouz_buffers* bufs);
+int ouz_init_state(ouz_env* env, void* stream);
+int ouz_step(ouz_env* env, const float* actions, void* stream);
+int ouz_step_n(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, void* stream);
+int ouz_reset_idx(ouz_env* env, const int32_t* env_ids, int32_t n, void* stream);
+int ouz_reset_all(ouz_env* env, void* stream);
+int64_t ouz_get_step(const ouz_env* env);
+int ouz_set_step(ouz_env* env, int64_t step);
+
+/* component entry points (same device functions as the fused step) */
+int ouz_lee_control(int32_t mode, const float* state, const float* cmd, float* thrust, float* torque, int32_t n,
+                    void* stream);
+int ouz_ekf_update(const float* q_wxyz, const float* P10, const float* gyr, const float* ang_wxyz, float dt,
+                   float* q_out, float* P10_out, int32_t n, void* stream);
+int ouz_pv_predict(float* x9, float* P45, const float* acc, const float* q_wxyz, float dt, int32_t n,
+                   void* stream);
+int ouz_pv_correct(float* x9, float* P45, const float* z, int32_t block, float var, const uint8_t* mask,
+                   int32_t n, void* stream);
+int ouz_integrate(float* root13, const float* f_b, const float* tau_b, const float* mass, const float* inertia,
+                  float dt, int32_t substeps, int32_t n, void* stream);
+int ouz_reward(const float* root13, const float* target, const int32_t* progress, int32_t max_episode_length,
+               float z_die, float* rew, int64_t* reset, int32_t n, void* stream);
+int ouz_philox(uint64_t seed, const uint32_t* env_ids, uint32_t step, uint32_t stream_id, uint32_t sub,
+               uint32_t* out4, int32_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OUZELUM_H_ */

@@ -1,0 +1,137 @@
+"""ctypes binding of ``libouzelum_hip.so`` (the C ABI declared in ``include/ouzelum.h``).
+
+This is the whole shim between Python and the HIP kernels: plain pointers
+and sizes cross it, nothing else.  There is no CPU fallback: if the shared
+library is missing or fails to load, importing this module raises
+``OuzelumError`` — the product path never silently runs anything else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so ours binds to the same libamdhip64
+
+LIB_NAME = "libouzelum_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+
+class OuzelumError(RuntimeError):
+    pass
+
+
+# --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
+ABI_VERSION = 1
+TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED = range(6)
+NUM_TASKS = 6
+POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
+LEE_POSITION, LEE_VELOCITY, LEE_ATTITUDE = range(3)
+NUM_OBS, NUM_ACT = 13, 4
+F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
+F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
+F_EP_RET, F_EP_SUM = 101, 102
+F_COUNT = 103
+I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT = range(8)
+I_COUNT = 8
+
+
+class OuzConfig(ctypes.Structure):
+    _fields_ = [
+        ("task", ctypes.c_int32), ("num_envs", ctypes.c_int32), ("env_id_offset", ctypes.c_int64),
+        ("num_envs_total", ctypes.c_int64), ("seed", ctypes.c_uint64), ("device", ctypes.c_int32),
+        ("pomdp", ctypes.c_int32), ("pomdp_prob", ctypes.c_float), ("dt", ctypes.c_float),
+        ("substeps", ctypes.c_int32), ("convergence_time", ctypes.c_int32), ("plat_speed", ctypes.c_float),
+        ("dr_lo", ctypes.c_float), ("dr_hi", ctypes.c_float), ("fault_eta_hi", ctypes.c_float),
+        ("thrust_max", ctypes.c_float), ("thrust_rate", ctypes.c_float), ("track_episodes", ctypes.c_int32),
+    ]
+
+
+class OuzBuffers(ctypes.Structure):
+    _fields_ = [("fstate", ctypes.c_void_p), ("istate", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("rew", ctypes.c_void_p), ("reset", ctypes.c_void_p), ("timeouts", ctypes.c_void_p)]
+
+
+class OuzTaskInfo(ctypes.Structure):
+    _fields_ = [("max_episode_length", ctypes.c_int32), ("z_die", ctypes.c_float), ("land_radius", ctypes.c_float),
+                ("pomdp", ctypes.c_int32), ("pomdp_prob", ctypes.c_float), ("uses_actions", ctypes.c_int32)]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int32
+_F = ctypes.c_float
+_U32 = ctypes.c_uint32
+_U64 = ctypes.c_uint64
+_I64 = ctypes.c_int64
+
+# name -> (restype, argtypes).  This table IS the list of symbols include/ouzelum.h declares.
+SIGNATURES = {
+    "ouz_abi_version": (_I, []),
+    "ouz_last_error": (ctypes.c_char_p, []),
+    "ouz_default_config": (None, [ctypes.POINTER(OuzConfig)]),
+    "ouz_task_info_get": (_I, [_I, ctypes.POINTER(OuzTaskInfo)]),
+    "ouz_create": (_I, [ctypes.POINTER(OuzConfig), ctypes.POINTER(_P)]),
+    "ouz_destroy": (_I, [_P]),
+    "ouz_bind": (_I, [_P, ctypes.POINTER(OuzBuffers)]),
+    "ouz_init_state": (_I, [_P, _P]),
+    "ouz_step": (_I, [_P, _P, _P]),
+    "ouz_step_n": (_I, [_P, _P, _I, _I, _P]),
+    "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
+    "ouz_reset_all": (_I, [_P, _P]),
+    "ouz_get_step": (_I64, [_P]),
+    "ouz_set_step": (_I, [_P, _I64]),
+    "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),
+    "ouz_ekf_update": (_I, [_P, _P, _P, _P, _F, _P, _P, _I, _P]),
+    "ouz_pv_predict": (_I, [_P, _P, _P, _P, _F, _I, _P]),
+    "ouz_pv_correct": (_I, [_P, _P, _P, _I, _F, _P, _I, _P]),
+    "ouz_integrate": (_I, [_P, _P, _P, _P, _P, _F, _I, _I, _P]),
+    "ouz_reward": (_I, [_P, _P, _P, _I, _F, _P, _P, _I, _P]),
+    "ouz_philox": (_I, [_U64, _P, _U32, _U32, _U32, _P, _I, _P]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise OuzelumError(
+            f"{LIB_NAME} not found at {LIB_PATH}: build it first (python -c 'import __graft_entry__ as g; g.build()'"
+            " or python -m ouzelum_amd.build). There is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the machine
+        raise OuzelumError(f"failed to load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ouz_abi_version() != ABI_VERSION:
+        raise OuzelumError(f"ABI mismatch: library {lib.ouz_abi_version()} != binding {ABI_VERSION}")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = lib.ouz_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        raise OuzelumError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_hip_tensor(t, name: str):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise OuzelumError(f"{name} must be a torch tensor on a HIP device (got {getattr(t, 'device', type(t))}); "
+                           "the HIP path has no CPU fallback")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")

@@ -1,0 +1,40 @@
+"""Build ``libouzelum_hip.so`` in-tree for gfx950 (explicit hipcc, no JIT cache).
+
+``python -m ouzelum_amd.build`` or ``__graft_entry__.build()``.  The library is
+written next to this file so it travels to the GPU box with the repo snapshot.
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "quad_kernels.hip")
+DEPS = [SRC, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc", "philox.h"),
+        os.path.join(ROOT, "include", "ouzelum.h")]
+OUT = os.path.join(HERE, "libouzelum_hip.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("OUZ_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and up_to_date():
+        return OUT
+    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,877 @@
+// Fused per-env quadrotor step for MI355X (gfx950) + the C ABI of include/ouzelum.h.
+//
+// Design:
+//  * one env per lane, wave64; per-env state is SoA f32 rows in HBM
+//    (fstate[field][env]) so every field load/store of a wave is one
+//    coalesced 256-byte transaction;
+//  * the whole VecTask.step — lazy reset, controller / estimator, wrench,
+//    2 integration sub-steps, reward/done/obs — is ONE kernel launch with no
+//    host synchronisation (the reference does reset_buf.nonzero() + per-env
+//    Python loops, ekf_lee_landed.py:312,378-444);
+//  * the task is a template parameter so each config compiles to straight-line
+//    code; the mixed curriculum assigns tasks per 64-env block, so every wave
+//    is task-uniform and the runtime switch never diverges inside a wave.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/ouzelum.h"
+#include "quad_math.h"
+
+namespace ouz {
+
+enum Ctrl { CTRL_RL = 0, CTRL_LEE_TRUE = 1, CTRL_LEE_EST = 2 };
+enum TargetMode { TGT_GOAL = 0, TGT_PLATFORM = 1, TGT_TRAJ = 2 };
+constexpr int kMixedChunk = 64;
+
+// Task presets — mirror oracle/quad_oracle.py::task_spec.
+struct TaskParams {
+  int32_t ctrl, target_mode, max_ep, pomdp;
+  float z_die, land_radius, plat_off_x, pomdp_prob;
+  float noise_lo, noise_hi;   // 1 -/+ sigma rounded to f32 (utils/POMDP.py:10)
+  int32_t land_vs_ctrl, dr, fault, motor_yaw;
+};
+
+static TaskParams task_preset(int task) {
+  TaskParams t{};
+  switch (task) {
+    case OUZ_TASK_OUZELUM:  // tasks/ouzelum.py, cfg/task/Ouzelum.yaml
+      t = TaskParams{CTRL_RL, TGT_GOAL, 2000, OUZ_POMDP_NONE, 0.5f, 0.0f, 0.0f, 0.0f, 1, 1, 0, 0, 0, 0};
+      break;
+    case OUZ_TASK_LEE_LANDED:  // tasks/lee_landed.py:25,263-330
+      t = TaskParams{CTRL_LEE_TRUE, TGT_PLATFORM, 2000, OUZ_POMDP_FLICKER, 0.3f, 0.2f, 0.08f, 0.01f, 1, 1, 1, 0, 0, 0};
+      break;
+    case OUZ_TASK_EKF_LEE_LANDED:  // tasks/ekf_lee_landed.py
+      t = TaskParams{CTRL_LEE_EST, TGT_PLATFORM, 700, OUZ_POMDP_FLICKER, 0.3f, 0.25f, -0.08f, 0.0f, 1, 1, 0, 0, 0, 0};
+      break;
+    case OUZ_TASK_TRACKING:
+      t = TaskParams{CTRL_LEE_EST, TGT_TRAJ, 700, OUZ_POMDP_FLICKER, 0.3f, 0.25f, -0.08f, 0.0f, 1, 1, 0, 1, 0, 0};
+      break;
+    case OUZ_TASK_FAULT:
+      t = TaskParams{CTRL_RL, TGT_GOAL, 2000, OUZ_POMDP_NOISE, 0.5f, 0.0f, 0.0f, 0.1f, 1, 1, 0, 0, 1, 1};
+      break;
+    default:
+      break;
+  }
+  return t;
+}
+
+struct EnvConsts {
+  float dt, thrust_step, thrust_max, plat_speed, dr_lo, dr_hi, fault_eta_hi, wmax;
+  int32_t substeps, conv_time;
+  float mass, ixx, iyy, izz;
+};
+
+struct StepArgs {
+  float* f;
+  int32_t* iv;
+  const float* actions;
+  float* obs;
+  float* rew;
+  int64_t* reset;
+  uint8_t* timeouts;
+  const float2* wp_tab;        // lemniscate[100] | circle[100] | square[4]
+  int32_t n;
+  uint32_t step;
+  uint32_t env_offset;
+  uint64_t n_total;
+  uint64_t seed;
+  uint32_t flick_mask;         // bit (task*8 + site): batch flicker coin fired this step
+  int32_t track_episodes;
+  EnvConsts c;
+  TaskParams tp[OUZ_NUM_TASKS];
+};
+
+// x500 lumped body (assets/x500/x500.urdf).  Rotor arms, x500.urdf:3-29.
+__device__ __constant__ float kRotorX[4] = {0.174f, -0.174f, 0.174f, -0.174f};
+__device__ __constant__ float kRotorY[4] = {-0.174f, 0.174f, 0.174f, -0.174f};
+__device__ __constant__ float kRotorDir[4] = {1.0f, 1.0f, -1.0f, -1.0f};   // ccw ccw cw cw (model.sdf:516-575)
+constexpr float kMotorKm = 0.016f;
+constexpr int kTrajLen[3] = {100, 100, 4};
+constexpr int kTrajBase[3] = {0, 100, 200};
+
+__device__ __forceinline__ int mixed_task(uint32_t gid) {
+  const int tasks[3] = {OUZ_TASK_LEE_LANDED, OUZ_TASK_TRACKING, OUZ_TASK_FAULT};
+  return tasks[(gid / kMixedChunk) % 3];
+}
+
+// ---------------------------------------------------------------------------
+// POMDP corruption (utils/POMDP.py:23-43) with counter-RNG draws
+// ---------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int task, const StepArgs& a,
+                                            uint32_t gid, uint32_t site, bool per_env_coin) {
+  const int mode = tp.pomdp;
+  if (mode == OUZ_POMDP_NONE) return;
+  if (mode == OUZ_POMDP_FLICKER || mode == OUZ_POMDP_FLICKER_NOISE) {
+    bool fire;
+    if (per_env_coin) {
+      const float p = (mode == OUZ_POMDP_FLICKER) ? tp.pomdp_prob : 0.1f;
+      fire = unit_f32(draw(a.seed, gid, a.step, RNG_POMDP + site, 0).x) <= p;
+    } else {
+      fire = (a.flick_mask >> (task * 8 + site)) & 1u;
+    }
+    if (fire) {
+#pragma unroll
+      for (int e = 0; e < D; ++e) x[e] = 0.0f;
+    }
+  }
+  if (mode == OUZ_POMDP_NOISE || mode == OUZ_POMDP_FLICKER_NOISE) {
+#pragma unroll
+    for (int g = 0; g < (D + 3) / 4; ++g) {
+      U4 r = draw(a.seed, gid, a.step, RNG_POMDP + site, 128 + g);
+      uint32_t w4[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (g * 4 + k < D) x[g * 4 + k] *= uniform_f32(w4[k], tp.noise_lo, tp.noise_hi);
+    }
+  }
+}
+
+__device__ __forceinline__ float ld(const StepArgs& a, int field, int i) { return a.f[(size_t)field * a.n + i]; }
+__device__ __forceinline__ void st(const StepArgs& a, int field, int i, float v) { a.f[(size_t)field * a.n + i] = v; }
+__device__ __forceinline__ int32_t ldi(const StepArgs& a, int field, int i) { return a.iv[(size_t)field * a.n + i]; }
+__device__ __forceinline__ void sti(const StepArgs& a, int field, int i, int32_t v) { a.iv[(size_t)field * a.n + i] = v; }
+__device__ __forceinline__ V3 ld3(const StepArgs& a, int f, int i) { return v3(ld(a, f, i), ld(a, f + 1, i), ld(a, f + 2, i)); }
+__device__ __forceinline__ void st3(const StepArgs& a, int f, int i, V3 v) { st(a, f, i, v.x); st(a, f + 1, i, v.y); st(a, f + 2, i, v.z); }
+
+__device__ __forceinline__ float2 traj_point(const StepArgs& a, int type, int idx, float sd) {
+  int len = type == 0 ? kTrajLen[0] : (type == 1 ? kTrajLen[1] : kTrajLen[2]);
+  int base = type == 0 ? kTrajBase[0] : (type == 1 ? kTrajBase[1] : kTrajBase[2]);
+  idx = idx < len - 1 ? idx : len - 1;
+  float2 p = a.wp_tab[base + idx];
+  return make_float2(p.x * sd, p.y * sd);
+}
+
+// ---------------------------------------------------------------------------
+// The fused step for one env (mirrors oracle/quad_oracle.py::OracleEnv.step)
+// ---------------------------------------------------------------------------
+template <int CTRL, int TGT>
+__device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid, int task) {
+  const TaskParams& tp = a.tp[task];
+  const EnvConsts& c = a.c;
+  const bool rst = a.reset[i] != 0;
+  V3 p = ld3(a, OUZ_F_P, i);
+  Q4 q{ld(a, OUZ_F_Q, i), ld(a, OUZ_F_Q + 1, i), ld(a, OUZ_F_Q + 2, i), ld(a, OUZ_F_Q + 3, i)};
+  V3 v = ld3(a, OUZ_F_V, i);
+  V3 w = ld3(a, OUZ_F_W, i);
+  int32_t progress = ldi(a, OUZ_I_PROGRESS, i);
+  int32_t land_flag = ldi(a, OUZ_I_LAND_FLAG, i);
+  V3 target = ld3(a, OUZ_F_TARGET, i);
+  float dr_m = 1.0f, dr_i = 1.0f, dr_t = 1.0f;
+  if (tp.dr) { dr_m = ld(a, OUZ_F_DR, i); dr_i = ld(a, OUZ_F_DR + 1, i); dr_t = ld(a, OUZ_F_DR + 2, i); }
+
+  // ---- lazy reset (ekf_lee_landed.py:271-306,312-335; ouzelum.py:192-233) ----
+  if (rst) {
+    U4 r = draw(a.seed, gid, a.step, RNG_RESET_POS);
+    p = v3(uniform_f32(r.x, -1.5f, 1.5f), uniform_f32(r.y, -1.5f, 1.5f), __fadd_rn(1.0f, uniform_f32(r.z, -0.2f, 1.5f)));
+    q = Q4{0.0f, 0.0f, 0.0f, 1.0f};
+    v = v3(0.0f, 0.0f, 0.0f);
+    w = v3(0.0f, 0.0f, 0.0f);
+    progress = 0;
+    sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + land_flag);
+    land_flag = 0;
+    if (tp.dr) {
+      U4 d = draw(a.seed, gid, a.step, RNG_DR);
+      dr_m = uniform_f32(d.x, c.dr_lo, c.dr_hi);
+      dr_i = uniform_f32(d.y, c.dr_lo, c.dr_hi);
+      dr_t = uniform_f32(d.z, c.dr_lo, c.dr_hi);
+      st(a, OUZ_F_DR, i, dr_m); st(a, OUZ_F_DR + 1, i, dr_i); st(a, OUZ_F_DR + 2, i, dr_t);
+    }
+    if (tp.fault) {
+      U4 d = draw(a.seed, gid, a.step, RNG_FAULT);
+      sti(a, OUZ_I_FAULT_ROTOR, i, (int32_t)(d.x >> 30));
+      st(a, OUZ_F_FAULT_ETA, i, uniform_f32(d.y, 0.0f, c.fault_eta_hi));
+      sti(a, OUZ_I_FAULT_ONSET, i, (int32_t)(d.z % (uint32_t)(tp.max_ep / 2 + 1)));
+    }
+  }
+
+  V3 f_b = v3(0.0f, 0.0f, 0.0f), tau_b = v3(0.0f, 0.0f, 0.0f);
+
+  if constexpr (CTRL == CTRL_RL) {
+    // ---- RL per-rotor thrust model (ouzelum.py:218-251) ----
+    if ((progress % 500) == 0 || rst) {   // set_targets (ouzelum.py:180-190)
+      U4 r = draw(a.seed, gid, a.step, RNG_TARGET);
+      target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
+                  __fadd_rn(unit_f32(r.z), 1.0f));
+    }
+    float4 act = reinterpret_cast<const float4*>(a.actions)[i];
+    float av[4] = {act.x, act.y, act.z, act.w};
+    float eff[4];
+    const bool on = tp.fault && progress >= ldi(a, OUZ_I_FAULT_ONSET, i);
+    const int frot = tp.fault ? ldi(a, OUZ_I_FAULT_ROTOR, i) : -1;
+    const float eta = tp.fault ? ld(a, OUZ_F_FAULT_ETA, i) : 1.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float ak = fminf(fmaxf(av[k], -1.0f), 1.0f);                 // vec_task.py:327
+      float th = ld(a, OUZ_F_THRUST + k, i) + c.thrust_step * ak;
+      th = fminf(fmaxf(th, 0.0f), c.thrust_max);                   // tensor_clamp
+      eff[k] = (on && frot == k) ? th * eta : th;
+      if (rst) { th = 0.0f; eff[k] = 0.0f; }                        // thrusts/forces[reset] = 0
+      st(a, OUZ_F_THRUST + k, i, th);
+    }
+    float tot = 0.0f, tx = 0.0f, ty = 0.0f, tz = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      tot += eff[k];
+      tx += eff[k] * kRotorY[k];
+      ty -= eff[k] * kRotorX[k];
+      tz -= eff[k] * (kMotorKm * kRotorDir[k]);
+    }
+    f_b = v3(0.0f, 0.0f, tot);
+    tau_b = v3(tx, ty, tp.motor_yaw ? tz : 0.0f);
+  } else if constexpr (CTRL == CTRL_LEE_TRUE) {
+    // ---- Lee on true state, hover at (0,0,1) (lee_landed.py:263-330) ----
+    float T;
+    V3 tau;
+    const V3 cmd = v3(0.0f, 0.0f, 1.0f);
+    lee_position(p, q, v, w, cmd, 0.0f, default_gains(), T, tau);
+    float fz = 2.0f * kGravity * T;
+    V3 dd = cmd - p;
+    if (sqrtf(dot(dd, dd)) < tp.land_radius) { land_flag = 1; fz = 0.0f; tau = v3(0.0f, 0.0f, 0.0f); }
+    if (rst) fz = 0.0f;                        // forces[reset] = 0, torques kept
+    f_b = v3(0.0f, 0.0f, fz * dr_t);
+    tau_b = tau;
+  } else {
+    // ---- AHRS-EKF + PV-KF + waypoint guidance + Lee (ekf_lee_landed.py:308-530) ----
+    const bool conv = a.step < (uint32_t)c.conv_time;
+    if constexpr (TGT == TGT_TRAJ) {
+      // kinematic stand-in for the husky waypoint follower (landing.py:319-364)
+      int ttype = ldi(a, OUZ_I_TRAJ_TYPE, i), tidx = ldi(a, OUZ_I_TRAJ_IDX, i);
+      float sd = ld(a, OUZ_F_TRAJ_SD, i);
+      float2 pl = make_float2(ld(a, OUZ_F_PLAT, i), ld(a, OUZ_F_PLAT + 1, i));
+      float2 wpp = traj_point(a, ttype, tidx, sd);
+      float dx = wpp.x - pl.x, dy = wpp.y - pl.y;
+      if (sqrtf(dx * dx + dy * dy) < 0.2f) tidx += 1;
+      int len = ttype == 0 ? kTrajLen[0] : (ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
+      if (tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
+        U4 r = draw(a.seed, gid, a.step, RNG_TRAJ);
+        ttype = (int)(r.x % 3u);
+        sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
+        tidx = 0;
+        sti(a, OUZ_I_TRAJ_TYPE, i, ttype);
+        st(a, OUZ_F_TRAJ_SD, i, sd);
+      }
+      sti(a, OUZ_I_TRAJ_IDX, i, tidx);
+      wpp = traj_point(a, ttype, tidx, sd);
+      dx = wpp.x - pl.x; dy = wpp.y - pl.y;
+      float d = sqrtf(dx * dx + dy * dy);
+      if (d > 0.0f) {
+        float s = fminf(c.plat_speed * c.dt, d) / d;
+        pl.x += dx * s; pl.y += dy * s;
+      }
+      st(a, OUZ_F_PLAT, i, pl.x); st(a, OUZ_F_PLAT + 1, i, pl.y);
+    }
+    V3 prev_v = ld3(a, OUZ_F_PREV_V, i);
+    V3 lin_acc = v3((v.x - prev_v.x) / c.dt, (v.y - prev_v.y) / c.dt, (v.z - prev_v.z) / c.dt);
+    lin_acc.z += 9.8f;                                 // aliasing quirk (ekf_lee_landed.py:366-367)
+    EkfQ qt{q.w, q.x, q.y, q.z};
+    EkfQ eq{ld(a, OUZ_F_EKF_Q, i), ld(a, OUZ_F_EKF_Q + 1, i), ld(a, OUZ_F_EKF_Q + 2, i), ld(a, OUZ_F_EKF_Q + 3, i)};
+    if (conv || rst) eq = qt;                          // :349-353
+    float px[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) px[k] = ld(a, OUZ_F_PV_X + k, i);
+    if (rst) { px[0] = p.x; px[1] = p.y; px[2] = p.z; px[3] = v.x; px[4] = v.y; px[5] = v.z; px[6] = px[7] = px[8] = 0.0f; }
+    float gyr[3] = {w.x, w.y, w.z};
+    float ang[4] = {qt.w, qt.x, qt.y, qt.z};
+    if (!conv) {
+      pomdp_apply<3>(gyr, tp, task, a, gid, SITE_GYR, false);
+      pomdp_apply<4>(ang, tp, task, a, gid, SITE_ANG, true);
+    }
+    float eP[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) eP[k] = ld(a, OUZ_F_EKF_P + k, i);
+    {
+      float inv = 1.0f / sqrtf(eq.w * eq.w + eq.x * eq.x + eq.y * eq.y + eq.z * eq.z);
+      eq = EkfQ{eq.w * inv, eq.x * inv, eq.y * inv, eq.z * inv};
+    }
+    ekf_update(eq, eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
+    EkfQ orient = eq;
+    float pm[3] = {p.x, p.y, p.z}, vm[3] = {v.x, v.y, v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
+    if (conv) {
+      orient = qt;
+    } else {
+      pomdp_apply<3>(am, tp, task, a, gid, SITE_ACC, false);
+      pomdp_apply<3>(pm, tp, task, a, gid, SITE_POS, false);
+      pomdp_apply<3>(vm, tp, task, a, gid, SITE_VEL, false);
+    }
+    float pP[45];
+#pragma unroll
+    for (int k = 0; k < 45; ++k) pP[k] = ld(a, OUZ_F_PV_P + k, i);
+    pv_predict(px, pP, v3(am[0], am[1], am[2]), orient, c.dt);
+    const uint64_t g = (uint64_t)a.step * a.n_total + gid;   // shared trigger counters (:425-440)
+    if (g % 7u == 6u) pv_correct<0>(px, pP, v3(pm[0], pm[1], pm[2]), kPvPosVar);
+    if (g % 3u == 0u) pv_correct<1>(px, pP, v3(vm[0], vm[1], vm[2]), 0.0f);   // R = 0 (PVFilter.py:76-79)
+    st3(a, OUZ_F_PREV_V, i, v);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_X + k, i, px[k]);
+#pragma unroll
+    for (int k = 0; k < 45; ++k) st(a, OUZ_F_PV_P + k, i, pP[k]);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, eP[k]);
+    st(a, OUZ_F_EKF_Q, i, eq.w); st(a, OUZ_F_EKF_Q + 1, i, eq.x); st(a, OUZ_F_EKF_Q + 2, i, eq.y); st(a, OUZ_F_EKF_Q + 3, i, eq.z);
+    // waypoint guidance (:464-492)
+    V3 wp = conv ? target : ld3(a, OUZ_F_WAYPOINT, i);
+    V3 tv = target - p;
+    float td = sqrtf(dot(tv, tv));
+    if (!conv) {
+      V3 wv = wp - p;
+      float wd = sqrtf(dot(wv, wv));
+      if (wd < 0.5f || wd > 1.0f) {
+        V3 vec = (target + v3(0.0f, 0.0f, 0.7f)) - p;
+        float nv = sqrtf(dot(vec, vec));
+        wp = v3(vec.x / nv * 0.75f + p.x, vec.y / nv * 0.75f + p.y, vec.z / nv * 0.75f + p.z);
+      }
+      if (td < 0.75f) wp = target + v3(0.0f, 0.0f, 0.09f);
+    }
+    st3(a, OUZ_F_WAYPOINT, i, wp);
+    float T;
+    V3 tau;
+    if (conv) lee_position(p, q, v, w, wp, 0.0f, default_gains(), T, tau);
+    else lee_position(v3(px[0], px[1], px[2]), q, v3(px[3], px[4], px[5]), w, wp, 0.0f, default_gains(), T, tau);
+    float fz = 2.0f * kGravity * T;
+    if (td < tp.land_radius) {                       // :508-515
+      if (!conv) land_flag = 1;
+      fz = 0.0f;
+      tau = v3(0.0f, 0.0f, 0.0f);
+    }
+    if (rst) fz = 0.0f;                              // :521
+    if (conv) { fz = 2.09f * kGravity; tau = v3(0.0f, 0.0f, 0.0f); }   // :526-530
+    f_b = v3(0.0f, 0.0f, fz * dr_t);
+    tau_b = tau;
+  }
+
+  // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
+  integrate(p, q, v, w, f_b, tau_b, c.mass * dr_m, v3(c.ixx * dr_i, c.iyy * dr_i, c.izz * dr_i), c.dt, c.substeps, c.wmax);
+
+  // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
+  progress += 1;
+  if constexpr (TGT == TGT_PLATFORM || TGT == TGT_TRAJ) {
+    float plx = 0.0f, ply = 0.0f;
+    if constexpr (TGT == TGT_TRAJ) { plx = ld(a, OUZ_F_PLAT, i); ply = ld(a, OUZ_F_PLAT + 1, i); }
+    target.x = plx + tp.plat_off_x;
+    target.y = ply;
+  }
+  float ob[13] = {(target.x - p.x) / 3.0f, (target.y - p.y) / 3.0f, (target.z - p.z) / 3.0f, q.x, q.y, q.z, q.w,
+                  v.x / 2.0f, v.y / 2.0f, v.z / 2.0f, w.x / kPiF, w.y / kPiF, w.z / kPiF};
+  pomdp_apply<13>(ob, tp, task, a, gid, SITE_OBS, false);
+  float dist;
+  float r = reward(p, target, q, w, dist);
+  const bool timeout_len = progress >= tp.max_ep - 1;
+  const bool die = dist > 8.0f || p.z < tp.z_die;
+  const bool rs = timeout_len || die;
+
+  // ---- stores ----
+  st3(a, OUZ_F_P, i, p);
+  st(a, OUZ_F_Q, i, q.x); st(a, OUZ_F_Q + 1, i, q.y); st(a, OUZ_F_Q + 2, i, q.z); st(a, OUZ_F_Q + 3, i, q.w);
+  st3(a, OUZ_F_V, i, v);
+  st3(a, OUZ_F_W, i, w);
+  st3(a, OUZ_F_TARGET, i, target);
+  sti(a, OUZ_I_PROGRESS, i, progress);
+  sti(a, OUZ_I_LAND_FLAG, i, land_flag);
+  float* o = a.obs + (size_t)i * OUZ_NUM_OBS;
+#pragma unroll
+  for (int k = 0; k < 13; ++k) o[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
+  a.rew[i] = r;
+  if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
+    float er = ld(a, OUZ_F_EP_RET, i) + r;
+    if (rs) {
+      st(a, OUZ_F_EP_SUM, i, ld(a, OUZ_F_EP_SUM, i) + er);
+      sti(a, OUZ_I_EP_CNT, i, ldi(a, OUZ_I_EP_CNT, i) + 1);
+      er = 0.0f;
+    }
+    st(a, OUZ_F_EP_RET, i, er);
+  }
+  a.reset[i] = rs ? 1 : 0;
+  a.timeouts[i] = (timeout_len && rs) ? 1 : 0;                             // vec_task.py:345
+}
+
+template <int TASK>
+__global__ void __launch_bounds__(256) quad_step_kernel(StepArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t gid = a.env_offset + (uint32_t)i;
+  if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
+    env_step<CTRL_RL, TGT_GOAL>(a, i, gid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
+    env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
+    env_step<CTRL_LEE_EST, TGT_PLATFORM>(a, i, gid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_TRACKING) {
+    env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, TASK);
+  } else {
+    const int t = mixed_task(gid);   // wave-uniform: 64-env blocks
+    if (t == OUZ_TASK_LEE_LANDED) env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, t);
+    else if (t == OUZ_TASK_TRACKING) env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, t);
+    else env_step<CTRL_RL, TGT_GOAL>(a, i, gid, t);
+  }
+}
+
+// Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
+__global__ void init_state_kernel(StepArgs a, int task_cfg) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t gid = a.env_offset + (uint32_t)i;
+  const int task = task_cfg == OUZ_TASK_MIXED ? mixed_task(gid) : task_cfg;
+  const TaskParams& tp = a.tp[task];
+  for (int k = 0; k < OUZ_F_COUNT; ++k) st(a, k, i, 0.0f);
+  for (int k = 0; k < OUZ_I_COUNT; ++k) sti(a, k, i, 0);
+  st(a, OUZ_F_P + 2, i, 1.0f);           // default_pose.p.z = 1 (ekf_lee_landed.py:228-229)
+  st(a, OUZ_F_Q + 3, i, 1.0f);
+  st(a, OUZ_F_TARGET + 2, i, tp.target_mode == TGT_GOAL ? 1.0f : 0.377f);   // ouzelum.py:73, ekf_lee_landed.py:87
+  st(a, OUZ_F_EKF_P + s4(0, 0), i, 1.0f); st(a, OUZ_F_EKF_P + s4(1, 1), i, 1.0f);   // ahrs_ekf.py:997
+  st(a, OUZ_F_EKF_P + s4(2, 2), i, 1.0f); st(a, OUZ_F_EKF_P + s4(3, 3), i, 1.0f);
+  for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_P + s9(k, k), i, kPvP0);        // PVFilter.py:12
+  st(a, OUZ_F_DR, i, 1.0f); st(a, OUZ_F_DR + 1, i, 1.0f); st(a, OUZ_F_DR + 2, i, 1.0f);
+  st(a, OUZ_F_FAULT_ETA, i, 1.0f);
+  if (tp.target_mode == TGT_TRAJ) {      // landing.py:209-213
+    U4 r = draw(a.seed, gid, INIT_STEP, RNG_TRAJ);
+    sti(a, OUZ_I_TRAJ_TYPE, i, (int)(r.x % 3u));
+    st(a, OUZ_F_TRAJ_SD, i, (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f));
+  }
+  for (int k = 0; k < OUZ_NUM_OBS; ++k) a.obs[(size_t)i * OUZ_NUM_OBS + k] = 0.0f;
+  a.rew[i] = 0.0f;
+  a.reset[i] = 1;                        // reset_buf starts at ones (vec_task.py:269-270)
+  a.timeouts[i] = 0;
+}
+
+__global__ void mark_reset_kernel(int64_t* reset, const int32_t* ids, int32_t n, int32_t n_envs) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) {
+    int32_t e = ids[k];
+    if (e >= 0 && e < n_envs) reset[e] = 1;
+  }
+}
+__global__ void mark_all_kernel(int64_t* reset, int32_t n) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) reset[k] = 1;
+}
+
+// ---------------------------------------------------------------------------
+// component kernels (AoS in/out; parity entry points)
+// ---------------------------------------------------------------------------
+__global__ void lee_kernel(int mode, const float* s, const float* cmd, float* thrust, float* torque, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* x = s + (size_t)i * 13;
+  const float* c = cmd + (size_t)i * 4;
+  V3 p = v3(x[0], x[1], x[2]), v = v3(x[7], x[8], x[9]), w = v3(x[10], x[11], x[12]);
+  Q4 q{x[3], x[4], x[5], x[6]};
+  float T;
+  V3 tau;
+  LeeGains g = default_gains();
+  if (mode == OUZ_LEE_POSITION) lee_position(p, q, v, w, v3(c[0], c[1], c[2]), c[3], g, T, tau);
+  else if (mode == OUZ_LEE_VELOCITY) lee_velocity(q, v, w, v3(c[0], c[1], c[2]), c[3], g, T, tau);
+  else lee_attitude(q, w, c[0], c[1], c[2], c[3], g, T, tau);
+  thrust[i] = T;
+  torque[i * 3 + 0] = tau.x; torque[i * 3 + 1] = tau.y; torque[i * 3 + 2] = tau.z;
+}
+
+__global__ void ekf_kernel(const float* q, const float* P, const float* gyr, const float* ang, float dt, float* qo,
+                           float* Po, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  EkfQ e{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]};
+  float p[10];
+  for (int k = 0; k < 10; ++k) p[k] = P[i * 10 + k];
+  ekf_update(e, p, v3(gyr[i * 3], gyr[i * 3 + 1], gyr[i * 3 + 2]), EkfQ{ang[i * 4], ang[i * 4 + 1], ang[i * 4 + 2], ang[i * 4 + 3]}, dt);
+  qo[i * 4] = e.w; qo[i * 4 + 1] = e.x; qo[i * 4 + 2] = e.y; qo[i * 4 + 3] = e.z;
+  for (int k = 0; k < 10; ++k) Po[i * 10 + k] = p[k];
+}
+
+__global__ void pv_predict_kernel(float* x, float* P, const float* acc, const float* q, float dt, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float xx[9], pp[45];
+  for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+  for (int k = 0; k < 45; ++k) pp[k] = P[i * 45 + k];
+  pv_predict(xx, pp, v3(acc[i * 3], acc[i * 3 + 1], acc[i * 3 + 2]), EkfQ{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]}, dt);
+  for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+  for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
+}
+
+__global__ void pv_correct_kernel(float* x, float* P, const float* z, int block, float var, const uint8_t* mask, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mask && !mask[i]) return;
+  float xx[9], pp[45];
+  for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+  for (int k = 0; k < 45; ++k) pp[k] = P[i * 45 + k];
+  V3 zz = v3(z[i * 3], z[i * 3 + 1], z[i * 3 + 2]);
+  if (block == 0) pv_correct<0>(xx, pp, zz, var);
+  else pv_correct<1>(xx, pp, zz, var);
+  for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+  for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
+}
+
+__global__ void integrate_kernel(float* root, const float* fb, const float* tb, const float* mass, const float* inertia,
+                                 float dt, int substeps, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* s = root + (size_t)i * 13;
+  V3 p = v3(s[0], s[1], s[2]), v = v3(s[7], s[8], s[9]), w = v3(s[10], s[11], s[12]);
+  Q4 q{s[3], s[4], s[5], s[6]};
+  integrate(p, q, v, w, v3(fb[i * 3], fb[i * 3 + 1], fb[i * 3 + 2]), v3(tb[i * 3], tb[i * 3 + 1], tb[i * 3 + 2]), mass[i],
+            v3(inertia[i * 3], inertia[i * 3 + 1], inertia[i * 3 + 2]), dt, substeps, 4.0f * kPiF);
+  s[0] = p.x; s[1] = p.y; s[2] = p.z; s[3] = q.x; s[4] = q.y; s[5] = q.z; s[6] = q.w;
+  s[7] = v.x; s[8] = v.y; s[9] = v.z; s[10] = w.x; s[11] = w.y; s[12] = w.z;
+}
+
+__global__ void reward_kernel(const float* root, const float* target, const int32_t* progress, int max_ep, float z_die,
+                              float* rew, int64_t* reset, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float* s = root + (size_t)i * 13;
+  float dist;
+  float r = reward(v3(s[0], s[1], s[2]), v3(target[i * 3], target[i * 3 + 1], target[i * 3 + 2]), Q4{s[3], s[4], s[5], s[6]},
+                   v3(s[10], s[11], s[12]), dist);
+  bool die = dist > 8.0f || s[2] < z_die;
+  rew[i] = r;
+  reset[i] = (progress[i] >= max_ep - 1 || die) ? 1 : 0;
+}
+
+__global__ void philox_kernel(uint64_t seed, const uint32_t* env, uint32_t step, uint32_t stream, uint32_t sub, uint32_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  U4 r = draw(seed, env[i], step, stream, sub);
+  out[i * 4] = r.x; out[i * 4 + 1] = r.y; out[i * 4 + 2] = r.z; out[i * 4 + 3] = r.w;
+}
+
+}  // namespace ouz
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace ouz;
+
+static_assert(sizeof(ouz_config) == 88, "ctypes OuzConfig mirror (ouzelum_amd/_lib.py)");
+static_assert(sizeof(ouz_buffers) == 48, "ctypes OuzBuffers mirror");
+static_assert(sizeof(ouz_task_info) == 24, "ctypes OuzTaskInfo mirror");
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(OUZ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return OUZ_OK;
+}
+inline int grid_for(int n, int block) { return (n + block - 1) / block; }
+inline int block_for(int n) { return n <= 65536 ? 64 : 256; }
+
+#define OUZ_LAUNCH_CHECK(what)                                         \
+  do {                                                                 \
+    hipError_t _e = hipGetLastError();                                 \
+    if (_e != hipSuccess) return hip_check(_e, what);                  \
+  } while (0)
+}  // namespace
+
+struct ouz_env {
+  ouz_config cfg;
+  ouz_buffers buf;
+  bool bound;
+  int64_t step;
+  float2* wp_tab;   // device waypoint tables
+  StepArgs args;    // pre-filled launch arguments
+};
+
+extern "C" {
+
+int32_t ouz_abi_version(void) { return OUZ_ABI_VERSION; }
+const char* ouz_last_error(void) { return g_err.c_str(); }
+
+void ouz_default_config(ouz_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->task = OUZ_TASK_LEE_LANDED;
+  c->num_envs = 4096;
+  c->pomdp = -1;
+  c->pomdp_prob = -1.0f;
+  c->dt = 0.01f;
+  c->substeps = 2;
+  c->convergence_time = 300;
+  c->plat_speed = 1.0f;
+  c->dr_lo = 0.9f;
+  c->dr_hi = 1.1f;
+  c->fault_eta_hi = 0.5f;
+  c->thrust_max = 2000.0f;
+  c->thrust_rate = 2000.0f;
+}
+
+int ouz_task_info_get(int32_t task, ouz_task_info* out) {
+  if (!out || task < 0 || task >= OUZ_NUM_TASKS) return fail(OUZ_ERR_INVALID, "ouz_task_info_get: bad task");
+  if (task == OUZ_TASK_MIXED) {
+    *out = ouz_task_info{2000, 0.3f, 0.2f, -1, -1.0f, 1};
+    return OUZ_OK;
+  }
+  TaskParams t = task_preset(task);
+  *out = ouz_task_info{t.max_ep, t.z_die, t.land_radius, t.pomdp, t.pomdp_prob, t.ctrl == CTRL_RL ? 1 : 0};
+  return OUZ_OK;
+}
+
+// Waypoint tables of landing.py:108-112 (lemniscate(a=4,100), circle(r=2,100), square(4,8)),
+// computed the way utils/trajectories.py:5-60 does (f32 theta for the lemniscate).
+static void build_waypoints(float2* tab) {
+  const double pi = 3.14159265358979323846;
+  for (int i = 0; i < 100; ++i) {
+    // torch.linspace(-pi/2, 3pi/2, 100) in f32
+    double step = (1.5 * pi - (-0.5 * pi)) / 99.0;
+    float th = (i < 50) ? (float)(-0.5 * pi + step * i) : (float)(1.5 * pi - step * (99 - i));
+    float s = sinf(th), c = cosf(th);
+    tab[i] = make_float2(4.0f * c / (s * s + 1.0f), 4.0f * c * s / (s * s + 1.0f));
+  }
+  for (int i = 0; i < 100; ++i) {
+    double ang = (i * (360.0 / 100.0)) * pi / 180.0;
+    tab[100 + i] = make_float2((float)(2.0 * std::cos(ang)), (float)(2.0 * std::sin(ang)));
+  }
+  const float sq[4][2] = {{0, 0}, {4, 0}, {4, 4}, {0, 4}};
+  for (int i = 0; i < 4; ++i) tab[200 + i] = make_float2(-(sq[i][0] - 2.0f), -(sq[i][1] - 2.0f));
+}
+
+int ouz_create(const ouz_config* cfg, ouz_env** out) {
+  if (!cfg || !out) return fail(OUZ_ERR_INVALID, "ouz_create: null argument");
+  if (cfg->task < 0 || cfg->task >= OUZ_NUM_TASKS) return fail(OUZ_ERR_INVALID, "ouz_create: unknown task");
+  if (cfg->num_envs <= 0) return fail(OUZ_ERR_INVALID, "ouz_create: num_envs must be > 0");
+  if (cfg->substeps <= 0 || !(cfg->dt > 0.0f)) return fail(OUZ_ERR_INVALID, "ouz_create: bad dt/substeps");
+  int64_t total = cfg->num_envs_total > 0 ? cfg->num_envs_total : cfg->num_envs;
+  if (cfg->env_id_offset < 0 || cfg->env_id_offset + cfg->num_envs > total || total > 0xFFFFFFFFll)
+    return fail(OUZ_ERR_INVALID, "ouz_create: env ids out of range");
+  int r = hip_check(hipSetDevice(cfg->device), "hipSetDevice");
+  if (r) return r;
+  ouz_env* e = new ouz_env();
+  e->cfg = *cfg;
+  e->cfg.num_envs_total = total;
+  e->bound = false;
+  e->step = 0;
+  float2 host_tab[204];
+  build_waypoints(host_tab);
+  r = hip_check(hipMalloc(&e->wp_tab, sizeof(host_tab)), "hipMalloc(waypoints)");
+  if (r) { delete e; return r; }
+  r = hip_check(hipMemcpy(e->wp_tab, host_tab, sizeof(host_tab), hipMemcpyHostToDevice), "hipMemcpy(waypoints)");
+  if (r) { hipFree(e->wp_tab); delete e; return r; }
+  StepArgs& a = e->args;
+  std::memset(&a, 0, sizeof(a));
+  a.wp_tab = e->wp_tab;
+  a.n = cfg->num_envs;
+  a.env_offset = (uint32_t)cfg->env_id_offset;
+  a.n_total = (uint64_t)total;
+  a.seed = cfg->seed;
+  a.track_episodes = cfg->track_episodes;
+  // x500 lumped mass properties (assets/x500/x500.urdf:31-35,98-177)
+  const double base_m = 2.0, rm = 0.016076923076923075;
+  const double mass = base_m + 4 * rm;
+  const double zc = 4 * rm * 0.3 / mass;
+  const double r_avg = 0.5 * (3.8464910483993325e-07 + 2.6115851691700804e-05);
+  double ixx = 0.02166666666666667 + base_m * zc * zc, izz = 0.04000000000000001;
+  const double rx[4] = {0.174, -0.174, 0.174, -0.174}, ry[4] = {-0.174, 0.174, 0.174, -0.174};
+  for (int k = 0; k < 4; ++k) {
+    ixx += r_avg + rm * (ry[k] * ry[k] + (0.3 - zc) * (0.3 - zc));
+    izz += 2.649858234714004e-05 + rm * (rx[k] * rx[k] + ry[k] * ry[k]);
+  }
+  a.c = EnvConsts{cfg->dt, (float)((double)cfg->dt * (double)cfg->thrust_rate), cfg->thrust_max, cfg->plat_speed,
+                  cfg->dr_lo, cfg->dr_hi, cfg->fault_eta_hi, (float)(4.0 * 3.14159265358979323846),
+                  cfg->substeps, cfg->convergence_time, (float)mass, (float)ixx, (float)ixx, (float)izz};
+  for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
+    TaskParams tp = task_preset(t);
+    if (cfg->pomdp >= 0) tp.pomdp = cfg->pomdp;
+    if (cfg->pomdp_prob >= 0.0f) tp.pomdp_prob = cfg->pomdp_prob;
+    double prob = (double)tp.pomdp_prob;
+    tp.noise_lo = (float)(1.0 - prob);
+    tp.noise_hi = (float)(1.0 + prob);
+    a.tp[t] = tp;
+  }
+  *out = e;
+  return OUZ_OK;
+}
+
+int ouz_destroy(ouz_env* env) {
+  if (!env) return OUZ_OK;
+  if (env->wp_tab) hipFree(env->wp_tab);
+  delete env;
+  return OUZ_OK;
+}
+
+int ouz_bind(ouz_env* env, const ouz_buffers* b) {
+  if (!env || !b) return fail(OUZ_ERR_INVALID, "ouz_bind: null argument");
+  if (!b->fstate || !b->istate || !b->obs || !b->rew || !b->reset || !b->timeouts)
+    return fail(OUZ_ERR_INVALID, "ouz_bind: every buffer pointer must be set");
+  env->buf = *b;
+  env->bound = true;
+  StepArgs& a = env->args;
+  a.f = b->fstate;
+  a.iv = b->istate;
+  a.obs = b->obs;
+  a.rew = b->rew;
+  a.reset = b->reset;
+  a.timeouts = b->timeouts;
+  return OUZ_OK;
+}
+
+int ouz_init_state(ouz_env* env, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_init_state: env not bound");
+  const int n = env->cfg.num_envs, blk = block_for(n);
+  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(n, blk)), dim3(blk), 0, (hipStream_t)stream, env->args,
+                     env->cfg.task);
+  OUZ_LAUNCH_CHECK("init_state_kernel");
+  env->step = 0;
+  return OUZ_OK;
+}
+
+// Whole-batch flicker coins (utils/POMDP.py:25: one torch.rand(1) per call) — identical for
+// every env, so they are drawn once per step here instead of once per lane.
+static uint32_t flicker_mask(const StepArgs& a, int cfg_task) {
+  uint32_t m = 0;
+  for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
+    if (cfg_task != OUZ_TASK_MIXED && t != cfg_task) continue;
+    const TaskParams& tp = a.tp[t];
+    if (tp.pomdp != OUZ_POMDP_FLICKER && tp.pomdp != OUZ_POMDP_FLICKER_NOISE) continue;
+    const float p = tp.pomdp == OUZ_POMDP_FLICKER ? tp.pomdp_prob : 0.1f;
+    for (uint32_t site = 0; site < 6; ++site) {
+      U4 r = draw(a.seed, BATCH_ENV, a.step, RNG_POMDP + site, (uint32_t)t);
+      if (unit_f32(r.x) <= p) m |= 1u << (t * 8 + site);
+    }
+  }
+  return m;
+}
+
+static int launch_step(ouz_env* env, const float* actions, hipStream_t s) {
+  StepArgs& a = env->args;
+  a.actions = actions;
+  a.step = (uint32_t)env->step;
+  a.flick_mask = flicker_mask(a, env->cfg.task);
+  const int n = env->cfg.num_envs, blk = block_for(n);
+  dim3 g(grid_for(n, blk)), b(blk);
+  switch (env->cfg.task) {
+    case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a); break;
+    case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a); break;
+    case OUZ_TASK_EKF_LEE_LANDED: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_EKF_LEE_LANDED>, g, b, 0, s, a); break;
+    case OUZ_TASK_TRACKING: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_TRACKING>, g, b, 0, s, a); break;
+    case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a); break;
+    default: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a); break;
+  }
+  OUZ_LAUNCH_CHECK("quad_step_kernel");
+  env->step += 1;
+  return OUZ_OK;
+}
+
+static bool needs_actions(int task) { return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_MIXED; }
+
+int ouz_step(ouz_env* env, const float* actions, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_step: env not bound");
+  if (!actions && needs_actions(env->cfg.task)) return fail(OUZ_ERR_INVALID, "ouz_step: this task needs actions");
+  if (actions && (reinterpret_cast<uintptr_t>(actions) & 15u)) return fail(OUZ_ERR_INVALID, "ouz_step: actions must be 16-byte aligned");
+  return launch_step(env, actions, (hipStream_t)stream);
+}
+
+int ouz_step_n(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_step_n: env not bound");
+  if (n_steps < 0 || (ring && ring_len <= 0)) return fail(OUZ_ERR_INVALID, "ouz_step_n: bad sizes");
+  if (!ring && needs_actions(env->cfg.task)) return fail(OUZ_ERR_INVALID, "ouz_step_n: this task needs actions");
+  for (int32_t k = 0; k < n_steps; ++k) {
+    const float* act = ring ? ring + (size_t)(k % ring_len) * env->cfg.num_envs * OUZ_NUM_ACT : nullptr;
+    int r = launch_step(env, act, (hipStream_t)stream);
+    if (r) return r;
+  }
+  return OUZ_OK;
+}
+
+int ouz_reset_idx(ouz_env* env, const int32_t* ids, int32_t n, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_reset_idx: env not bound");
+  if (n < 0 || (n > 0 && !ids)) return fail(OUZ_ERR_INVALID, "ouz_reset_idx: bad ids");
+  if (n == 0) return OUZ_OK;
+  hipLaunchKernelGGL(mark_reset_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, env->buf.reset, ids, n,
+                     env->cfg.num_envs);
+  OUZ_LAUNCH_CHECK("mark_reset_kernel");
+  return OUZ_OK;
+}
+
+int ouz_reset_all(ouz_env* env, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_reset_all: env not bound");
+  const int n = env->cfg.num_envs;
+  hipLaunchKernelGGL(mark_all_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, env->buf.reset, n);
+  OUZ_LAUNCH_CHECK("mark_all_kernel");
+  return OUZ_OK;
+}
+
+int64_t ouz_get_step(const ouz_env* env) { return env ? env->step : -1; }
+int ouz_set_step(ouz_env* env, int64_t step) {
+  if (!env || step < 0 || step > 0xFFFFFFFFll) return fail(OUZ_ERR_INVALID, "ouz_set_step: bad step");
+  env->step = step;
+  return OUZ_OK;
+}
+
+#define OUZ_CHECK_N(fn)                                                    \
+  if (n < 0) return fail(OUZ_ERR_INVALID, fn ": n must be >= 0");          \
+  if (n == 0) return OUZ_OK;
+
+int ouz_lee_control(int32_t mode, const float* state, const float* cmd, float* thrust, float* torque, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_lee_control");
+  if (mode < 0 || mode > 2) return fail(OUZ_ERR_INVALID, "ouz_lee_control: Invalid controller name");
+  if (!state || !cmd || !thrust || !torque) return fail(OUZ_ERR_INVALID, "ouz_lee_control: null pointer");
+  hipLaunchKernelGGL(lee_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, mode, state, cmd, thrust, torque, n);
+  OUZ_LAUNCH_CHECK("lee_kernel");
+  return OUZ_OK;
+}
+
+int ouz_ekf_update(const float* q, const float* P, const float* gyr, const float* ang, float dt, float* qo, float* Po,
+                   int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_ekf_update");
+  if (!q || !P || !gyr || !ang || !qo || !Po) return fail(OUZ_ERR_INVALID, "ouz_ekf_update: null pointer");
+  hipLaunchKernelGGL(ekf_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, q, P, gyr, ang, dt, qo, Po, n);
+  OUZ_LAUNCH_CHECK("ekf_kernel");
+  return OUZ_OK;
+}
+
+int ouz_pv_predict(float* x, float* P, const float* acc, const float* q, float dt, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_pv_predict");
+  if (!x || !P || !acc || !q) return fail(OUZ_ERR_INVALID, "ouz_pv_predict: null pointer");
+  hipLaunchKernelGGL(pv_predict_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, x, P, acc, q, dt, n);
+  OUZ_LAUNCH_CHECK("pv_predict_kernel");
+  return OUZ_OK;
+}
+
+int ouz_pv_correct(float* x, float* P, const float* z, int32_t block, float var, const uint8_t* mask, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_pv_correct");
+  if (!x || !P || !z) return fail(OUZ_ERR_INVALID, "ouz_pv_correct: null pointer");
+  if (block != 0 && block != 1) return fail(OUZ_ERR_INVALID, "ouz_pv_correct: block must be 0 (position) or 1 (velocity)");
+  hipLaunchKernelGGL(pv_correct_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, x, P, z, block, var, mask, n);
+  OUZ_LAUNCH_CHECK("pv_correct_kernel");
+  return OUZ_OK;
+}
+
+int ouz_integrate(float* root, const float* fb, const float* tb, const float* mass, const float* inertia, float dt,
+                  int32_t substeps, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_integrate");
+  if (!root || !fb || !tb || !mass || !inertia || substeps <= 0) return fail(OUZ_ERR_INVALID, "ouz_integrate: bad argument");
+  hipLaunchKernelGGL(integrate_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, root, fb, tb, mass, inertia, dt,
+                     substeps, n);
+  OUZ_LAUNCH_CHECK("integrate_kernel");
+  return OUZ_OK;
+}
+
+int ouz_reward(const float* root, const float* target, const int32_t* progress, int32_t max_ep, float z_die, float* rew,
+               int64_t* reset, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_reward");
+  if (!root || !target || !progress || !rew || !reset) return fail(OUZ_ERR_INVALID, "ouz_reward: null pointer");
+  hipLaunchKernelGGL(reward_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, root, target, progress, max_ep,
+                     z_die, rew, reset, n);
+  OUZ_LAUNCH_CHECK("reward_kernel");
+  return OUZ_OK;
+}
+
+int ouz_philox(uint64_t seed, const uint32_t* env_ids, uint32_t step, uint32_t stream_id, uint32_t sub, uint32_t* out4,
+               int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_philox");
+  if (!env_ids || !out4) return fail(OUZ_ERR_INVALID, "ouz_philox: null pointer");
+  hipLaunchKernelGGL(philox_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, seed, env_ids, step, stream_id, sub,
+                     out4, n);
+  OUZ_LAUNCH_CHECK("philox_kernel");
+  return OUZ_OK;
+}
+
+}  // extern "C"

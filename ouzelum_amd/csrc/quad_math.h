@@ -1,0 +1,496 @@
+// Per-env quadrotor math for the fused step kernel (gfx950, one env per lane).
+//
+// Everything here is register-resident f32 scalar code: 3x3 / 4x4 / 9x9 work is
+// far too small for MFMA (no dense contraction on this path), so it
+// is written as straight-line VALU math that the compiler keeps in VGPRs.
+//
+// Each function names the reference routine it restates.  Where the reference
+// evaluates an ill-conditioned Kalman update literally — (I - K H) P with
+// R = 1e-7 against P = O(1..1000) — the algebraically identical, f32-stable
+// form is used instead (derivations in DESIGN.md §4); the literal float64 form
+// lives in the CPU oracle, pinned against the reference's own modules.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "philox.h"
+
+namespace ouz {
+
+// ---------------------------------------------------------------------------
+// small vector / matrix types
+// ---------------------------------------------------------------------------
+struct V3 { float x, y, z; };
+struct Q4 { float x, y, z, w; };          // xyzw (Isaac root-state order)
+struct M3 { float m[9]; };                 // row-major
+
+OUZ_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+OUZ_HD V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+OUZ_HD V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+OUZ_HD V3 operator*(float s, V3 a) { return V3{s * a.x, s * a.y, s * a.z}; }
+OUZ_HD V3 mul(V3 a, V3 b) { return V3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+OUZ_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+OUZ_HD V3 cross(V3 a, V3 b) { return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+OUZ_HD float norm(V3 a) { return sqrtf(dot(a, a)); }
+
+OUZ_HD V3 mv(const M3& A, V3 v) {
+  return V3{A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
+            A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z};
+}
+OUZ_HD V3 mtv(const M3& A, V3 v) {  // A^T v
+  return V3{A.m[0] * v.x + A.m[3] * v.y + A.m[6] * v.z, A.m[1] * v.x + A.m[4] * v.y + A.m[7] * v.z,
+            A.m[2] * v.x + A.m[5] * v.y + A.m[8] * v.z};
+}
+OUZ_HD M3 mm(const M3& A, const M3& B) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C.m[i * 3 + j] = A.m[i * 3 + 0] * B.m[0 * 3 + j] + A.m[i * 3 + 1] * B.m[1 * 3 + j] + A.m[i * 3 + 2] * B.m[2 * 3 + j];
+  return C;
+}
+OUZ_HD M3 mmt(const M3& A, const M3& B) {  // A B^T
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      C.m[i * 3 + j] = A.m[i * 3 + 0] * B.m[j * 3 + 0] + A.m[i * 3 + 1] * B.m[j * 3 + 1] + A.m[i * 3 + 2] * B.m[j * 3 + 2];
+  return C;
+}
+OUZ_HD M3 tr(const M3& A) {
+  M3 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C.m[i * 3 + j] = A.m[j * 3 + i];
+  return C;
+}
+OUZ_HD M3 madd(const M3& A, const M3& B) { M3 C;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] + B.m[k]; return C; }
+OUZ_HD M3 msub(const M3& A, const M3& B) { M3 C;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] - B.m[k]; return C; }
+OUZ_HD M3 mscale(float s, const M3& A) { M3 C;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) C.m[k] = s * A.m[k]; return C; }
+
+// Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).
+OUZ_HD M3 inv_sym3(const M3& S) {
+  float a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
+  float A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
+  float D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
+  float inv_det = 1.0f / (a * A + b * B + c * C);
+  return M3{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
+             C * inv_det, E * inv_det, F * inv_det}};
+}
+
+// ---------------------------------------------------------------------------
+// rotations
+// ---------------------------------------------------------------------------
+// quaternion_to_matrix on the wxyz reorder of an xyzw quaternion
+// (controllers/rotation_conversions.py:36-64; position_control.py:28-29).
+OUZ_HD M3 quat_to_mat(Q4 q) {
+  float r = q.w, i = q.x, j = q.y, k = q.z;
+  float two_s = 2.0f / (r * r + i * i + j * j + k * k);
+  return M3{{1.0f - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+             two_s * (i * j + k * r), 1.0f - two_s * (i * i + k * k), two_s * (j * k - i * r),
+             two_s * (i * k - j * r), two_s * (j * k + i * r), 1.0f - two_s * (i * i + j * j)}};
+}
+
+// matrix_to_euler_angles(R, "ZYX")[:, [2,1,0]] (rotation_conversions.py:216-255).
+OUZ_HD void mat_to_rpy(const M3& R, float& roll, float& pitch, float& yaw) {
+  roll = atan2f(R.m[7], R.m[8]);
+  pitch = asinf(-R.m[6]);
+  yaw = atan2f(R.m[3], R.m[0]);
+}
+
+// euler_angles_to_matrix((yaw, pitch, roll), "ZYX") = Rz Ry Rx (rotation_conversions.py:149-171).
+OUZ_HD M3 rpy_to_mat(float yaw, float pitch, float roll) {
+  float cz = cosf(yaw), sz = sinf(yaw), cy = cosf(pitch), sy = sinf(pitch), cx = cosf(roll), sx = sinf(roll);
+  return M3{{cz * cy, cz * sy * sx - sz * cx, cz * sy * cx + sz * sx, sz * cy, sz * sy * sx + cz * cx,
+             sz * sy * cx - cz * sx, -sy, cy * sx, cy * cx}};
+}
+
+// my_quat_rotate / quat_rotate, xyzw (utils/torch_jit_utils.py:198-208).
+OUZ_HD V3 quat_rotate(Q4 q, V3 v) {
+  V3 qv = v3(q.x, q.y, q.z);
+  V3 a = (2.0f * q.w * q.w - 1.0f) * v;
+  V3 b = (q.w * 2.0f) * cross(qv, v);
+  V3 c = (dot(qv, v) * 2.0f) * qv;
+  return a + b + c;
+}
+
+OUZ_HD Q4 quat_mul(Q4 a, Q4 b) {  // xyzw Hamilton product a (x) b
+  return Q4{a.w * b.x + b.w * a.x + (a.y * b.z - a.z * b.y), a.w * b.y + b.w * a.y + (a.z * b.x - a.x * b.z),
+            a.w * b.z + b.w * a.z + (a.x * b.y - a.y * b.x), a.w * b.w - (a.x * b.x + a.y * b.y + a.z * b.z)};
+}
+
+// ---------------------------------------------------------------------------
+// Lee geometric controllers
+// ---------------------------------------------------------------------------
+struct LeeGains { V3 kP, kV, kR, kW; };
+
+OUZ_HD LeeGains default_gains() {  // controllers/control_config.py:14-17
+  return LeeGains{v3(0.8f, 0.8f, 1.0f), v3(0.5f, 0.5f, 0.4f), v3(3.0f, 3.0f, 1.0f), v3(0.5f, 0.5f, 1.2f)};
+}
+
+constexpr float kTwoPiF = 6.28318530717958647692f;
+constexpr float kPiF = 3.14159265358979323846f;
+
+// torch.remainder for floats: fmod, then shift into the divisor's sign.
+OUZ_HD float remainder_f(float a, float b) {
+  float m = fmodf(a, b);
+  if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
+  return m;
+}
+
+// Shared attitude loop (position_control.py:66-108): returns torque.
+OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, float roll, float pitch, float yaw_rate,
+                            const LeeGains& g) {
+  // A = Rd^T R ; vee(A - A^T) = (A21 - A12, A02 - A20, A10 - A01)
+  M3 A;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A.m[i * 3 + j] = Rd.m[0 * 3 + i] * R.m[0 * 3 + j] + Rd.m[1 * 3 + i] * R.m[1 * 3 + j] + Rd.m[2 * 3 + i] * R.m[2 * 3 + j];
+  V3 e_R = v3(0.5f * (A.m[7] - A.m[5]), 0.5f * (A.m[2] - A.m[6]), 0.5f * (A.m[3] - A.m[1]));
+  float sp = sinf(pitch), cp = cosf(pitch), sr = sinf(roll), cr = cosf(roll);
+  V3 wd = v3(-sp * yaw_rate, sr * cp * yaw_rate, cr * cp * yaw_rate);
+  V3 des = mtv(R, mv(Rd, wd));
+  V3 act = mtv(R, omega);
+  V3 e_w = act - des;
+  // + cross(w, w) == 0 (position_control.py:108)
+  return v3(-g.kR.x * e_R.x - g.kW.x * e_w.x, -g.kR.y * e_R.y - g.kW.y * e_w.y, -g.kR.z * e_R.z - g.kW.z * e_w.z);
+}
+
+// LeePositionController.__call__ (controllers/position_control.py:19-109).
+// cmd = (x, y, z, yaw); thrust in units of m*g, torque "inertia normalised".
+OUZ_HD void lee_position(V3 p, Q4 q, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const LeeGains& g, float& thrust,
+                         V3& torque) {
+  M3 R = quat_to_mat(q);
+  float roll, pitch, yaw;
+  mat_to_rpy(R, roll, pitch, yaw);
+  V3 a = mul(g.kP, cmd_p - p) - mul(g.kV, v);
+  a.z += 1.0f;
+  thrust = a.x * R.m[2] + a.y * R.m[5] + a.z * R.m[8];
+  float na = norm(a);
+  V3 b3 = v3(a.x / na, a.y / na, a.z / na);
+  V3 c = v3(cosf(yaw), sinf(yaw), 0.0f);
+  V3 b2 = cross(b3, c);
+  float nb = norm(b2);
+  b2 = v3(b2.x / nb, b2.y / nb, b2.z / nb);
+  V3 b1 = cross(b2, b3);
+  M3 Rd{{b1.x, b2.x, b3.x, b1.y, b2.y, b3.y, b1.z, b2.z, b3.z}};
+  float yr = remainder_f(cmd_yaw - yaw, kTwoPiF);
+  if (yr > kPiF) yr -= kTwoPiF;
+  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yr, g);
+}
+
+// LeeVelocityController.__call__ (controllers/velocity_control.py:17-112).
+OUZ_HD void lee_velocity(Q4 q, V3 v, V3 w, V3 cmd_v, float yaw_rate, const LeeGains& g, float& thrust,
+                         V3& torque) {
+  M3 R = quat_to_mat(q);
+  float roll, pitch, yaw;
+  mat_to_rpy(R, roll, pitch, yaw);
+  M3 Rv = rpy_to_mat(yaw, 0.0f, 0.0f);
+  V3 vv = mtv(Rv, v);
+  V3 a = mul(g.kV, cmd_v - vv);
+  a.z += 1.0f;
+  thrust = a.x * R.m[2] + a.y * R.m[5] + a.z * R.m[8];
+  float pitch_sp = atan2f(a.x, a.z);
+  float roll_sp = atan2f(-a.y, sqrtf(a.z * a.z + a.x * a.x));
+  M3 Rd = rpy_to_mat(yaw, pitch_sp, roll_sp);
+  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yaw_rate, g);
+}
+
+// LeeAttitudeContoller.__call__ (controllers/attitude_control.py:17-78): cmd = (T, roll, pitch, yaw_rate).
+OUZ_HD void lee_attitude(Q4 q, V3 w, float cmd_t, float cmd_roll, float cmd_pitch, float yaw_rate,
+                         const LeeGains& g, float& thrust, V3& torque) {
+  M3 R = quat_to_mat(q);
+  float roll, pitch, yaw;
+  mat_to_rpy(R, roll, pitch, yaw);
+  M3 Rd = rpy_to_mat(yaw, cmd_pitch, cmd_roll);
+  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yaw_rate, g);
+  thrust = cmd_t + 1.0f;
+}
+
+// ---------------------------------------------------------------------------
+// AHRS-EKF, executed "ang" branch (ahrs_ekf.py:1301-1337), SURVEY a12.
+// q = (w, x, y, z) scalar-first; P symmetric 4x4 packed (00,01,02,03,11,12,13,22,23,33).
+// ---------------------------------------------------------------------------
+struct EkfQ { float w, x, y, z; };
+
+OUZ_HD int s4(int i, int j) {  // packed index, any order
+  int a = i < j ? i : j, b = i < j ? j : i;
+  return a * 4 - (a * (a - 1)) / 2 + (b - a);
+}
+
+// Full symmetric 4x4 inverse via Cholesky (S is SPD: P_t + 1e-7 I).
+OUZ_HD void inv_spd4(const float S[10], float Si[10]) {
+  float L[4][4] = {};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float d = S[s4(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
+    float ljj = sqrtf(d);
+    L[j][j] = ljj;
+    float inv = 1.0f / ljj;
+#pragma unroll
+    for (int i = j + 1; i < 4; ++i) {
+      float s = S[s4(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
+      L[i][j] = s * inv;
+    }
+  }
+  // Linv (lower)
+  float Li[4][4] = {};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    Li[i][i] = 1.0f / L[i][i];
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = j; k < i; ++k) s += L[i][k] * Li[k][j];
+      Li[i][j] = -s * Li[i][i];
+    }
+  }
+  // S^-1 = Linv^T Linv
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = i; j < 4; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = j; k < 4; ++k) s += Li[k][i] * Li[k][j];
+      Si[s4(i, j)] = s;
+    }
+}
+
+constexpr float kEkfGNoise = 0.09f;   // 0.3**2, ahrs_ekf.py:1004
+constexpr float kEkfAngR = 1e-7f;      // ahrs_ekf.py:1332
+
+// In: q (normalised prior), P. Out: q, P updated in place.
+OUZ_HD void ekf_update(EkfQ& q, float P[10], V3 g, EkfQ ang, float Dt) {
+  const float h = 0.5f * Dt;
+  // Omega(x) rows (ahrs_ekf.py:1072-1106)
+  float O[4][4] = {{0.0f, -g.x, -g.y, -g.z}, {g.x, 0.0f, g.z, -g.y}, {g.y, -g.z, 0.0f, g.x}, {g.z, g.y, -g.x, 0.0f}};
+  float qv[4] = {q.w, q.x, q.y, q.z};
+  float qt[4];
+  float F[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float fij = (i == j ? 1.0f : 0.0f) + h * O[i][j];   // f(): (I + 0.5 Dt Omega(g)) q
+      s += fij * qv[j];
+      F[i][j] = (i == j ? 1.0f : 0.0f) + O[i][j] * h;     // dfdq: I + Omega(0.5 Dt g)
+    }
+    qt[i] = s;
+  }
+  // W = 0.5 Dt [ -q_v^T ; q_w I + skew(q_v) ]   (4x3), Q_t = 0.5 Dt g_noise W W^T
+  float W[4][3] = {{-q.x, -q.y, -q.z}, {q.w, -q.z, q.y}, {q.z, q.w, -q.x}, {-q.y, q.x, q.w}};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) W[i][j] *= h;
+  // FP (4x4 full)
+  float FP[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += F[i][k] * P[s4(k, j)];
+      FP[i][j] = s;
+    }
+  float Pt[10];
+  const float qs = h * kEkfGNoise;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = i; j < 4; ++j) {
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += FP[i][k] * F[j][k];
+      float ww = W[i][0] * W[j][0] + W[i][1] * W[j][1] + W[i][2] * W[j][2];
+      Pt[s4(i, j)] = s + qs * ww;
+    }
+  // S = P_t + r I ; stable identities:
+  //   (I - K) P_t = r I - r^2 S^-1 ,  q_t + K v = ang - r S^-1 v
+  float S[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) S[k] = Pt[k];
+  S[s4(0, 0)] += kEkfAngR; S[s4(1, 1)] += kEkfAngR; S[s4(2, 2)] += kEkfAngR; S[s4(3, 3)] += kEkfAngR;
+  float Si[10];
+  inv_spd4(S, Si);
+  float av[4] = {ang.w, ang.x, ang.y, ang.z};
+  float vv[4] = {av[0] - qt[0], av[1] - qt[1], av[2] - qt[2], av[3] - qt[3]};
+  float qn[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += Si[s4(i, j)] * vv[j];
+    qn[i] = av[i] - kEkfAngR * s;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = i; j < 4; ++j) P[s4(i, j)] = (i == j ? kEkfAngR : 0.0f) - (kEkfAngR * kEkfAngR) * Si[s4(i, j)];
+  float inv = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+  q = EkfQ{qn[0] * inv, qn[1] * inv, qn[2] * inv, qn[3] * inv};
+}
+
+// ---------------------------------------------------------------------------
+// Position/velocity KF (PVFilter.py:25-110), SURVEY a13.
+// x = [p, v, b_a]; P symmetric 9x9 packed upper triangle (45 floats).
+// ---------------------------------------------------------------------------
+OUZ_HD constexpr int s9(int i, int j) {
+  return (i <= j) ? (i * 9 - (i * (i - 1)) / 2 + (j - i)) : (j * 9 - (j * (j - 1)) / 2 + (i - j));
+}
+
+// 3x3 block (bi, bj) of the packed 9x9 (bi, bj in 0..2).
+OUZ_HD M3 pblk(const float P[45], int bi, int bj) {
+  M3 B;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) B.m[i * 3 + j] = P[s9(bi * 3 + i, bj * 3 + j)];
+  return B;
+}
+// Store block (bi <= bj); for a diagonal block only its upper triangle is kept.
+OUZ_HD void pset(float P[45], int bi, int bj, const M3& B) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (bi != bj || i <= j) P[s9(bi * 3 + i, bj * 3 + j)] = B.m[i * 3 + j];
+}
+
+constexpr float kPvAccVar = 1.0f;     // [0.01]*3 * 100 (ekf_lee_landed.py:137)
+constexpr float kPvPosVar = 1e-7f;    // ekf_lee_landed.py:408
+constexpr float kPvP0 = 1000.0f;      // PVFilter.py:12
+
+// prediction_step: M = R(q/|q|)^T; F = [[I, M dt, M h],[0, M, M dt],[0,0,I]], G = F[:, 6:9] (rows 0..5),
+// x = F x + G (a - b); P = F P F^T + q_a G G^T.   (h = dt^2/2)
+OUZ_HD void pv_predict(float x[9], float P[45], V3 acc, EkfQ q, float dt) {
+  float inv = 1.0f / sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+  M3 M = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
+  const float h = dt * dt * 0.5f;
+  V3 xp = v3(x[0], x[1], x[2]), xv = v3(x[3], x[4], x[5]), xb = v3(x[6], x[7], x[8]);
+  V3 u = acc - xb;
+  V3 np_ = xp + mv(M, dt * xv) + mv(M, h * xb) + mv(M, h * u);
+  V3 nv = mv(M, xv) + mv(M, dt * xb) + mv(M, dt * u);
+  x[0] = np_.x; x[1] = np_.y; x[2] = np_.z;
+  x[3] = nv.x; x[4] = nv.y; x[5] = nv.z;
+  // block algebra
+  M3 P11 = pblk(P, 0, 0), P12 = pblk(P, 0, 1), P13 = pblk(P, 0, 2);
+  M3 P22 = pblk(P, 1, 1), P23 = pblk(P, 1, 2), P33 = pblk(P, 2, 2);
+  M3 P21 = tr(P12), P31 = tr(P13), P32 = tr(P23);
+  M3 T13 = madd(P13, mm(M, madd(mscale(dt, P23), mscale(h, P33))));
+  M3 T12 = madd(P12, mm(M, madd(mscale(dt, P22), mscale(h, P32))));
+  M3 T11 = madd(P11, mm(M, madd(mscale(dt, P21), mscale(h, P31))));
+  M3 T23 = mm(M, madd(P23, mscale(dt, P33)));
+  M3 T22 = mm(M, madd(P22, mscale(dt, P32)));
+  M3 MMt = mmt(M, M);
+  M3 N11 = madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(kPvAccVar * h * h, MMt));
+  M3 N12 = madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(kPvAccVar * h * dt, MMt));
+  M3 N22 = madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(kPvAccVar * dt * dt, MMt));
+  pset(P, 0, 0, N11); pset(P, 0, 1, N12); pset(P, 0, 2, T13);
+  pset(P, 1, 1, N22); pset(P, 1, 2, T23);
+}
+
+// correction_step for one measured block m (0 = position, 1 = velocity) with R = r I.
+// Stable form of x += K (z - x_m); P = (I - K H) P  (DESIGN.md §4):
+//   S = P_mm + r I;  K_o = P_om S^-1 (o != m)
+//   x_m = z - r S^-1 y;  x_o += K_o y
+//   P_mm = r (I - r S^-1);  P_mo = r S^-1 P_mo;  P_oo' = P_oo' - K_o P_mo'
+template <int MB>
+OUZ_HD void pv_correct(float x[9], float P[45], V3 z, float r) {
+  constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
+  constexpr int B = 2;
+  M3 Pmm = pblk(P, MB, MB);
+  M3 S = Pmm;
+  S.m[0] += r; S.m[4] += r; S.m[8] += r;
+  M3 Si = inv_sym3(S);
+  M3 PmA = pblk(P, MB, A), PmB = pblk(P, MB, B);     // P_{m,o}
+  M3 KA = mm(tr(PmA), Si), KB = mm(tr(PmB), Si);     // K_o = P_{o,m} S^-1
+  V3 xm = v3(x[MB * 3 + 0], x[MB * 3 + 1], x[MB * 3 + 2]);
+  V3 y = z - xm;
+  V3 nm = z - r * mv(Si, y);
+  V3 dA = mv(KA, y), dB = mv(KB, y);
+  x[MB * 3 + 0] = nm.x; x[MB * 3 + 1] = nm.y; x[MB * 3 + 2] = nm.z;
+  x[A * 3 + 0] += dA.x; x[A * 3 + 1] += dA.y; x[A * 3 + 2] += dA.z;
+  x[B * 3 + 0] += dB.x; x[B * 3 + 1] += dB.y; x[B * 3 + 2] += dB.z;
+  M3 PAA = pblk(P, A, A), PAB = pblk(P, A, B), PBB = pblk(P, B, B);
+  M3 nAA = msub(PAA, mm(KA, PmA));
+  M3 nAB = msub(PAB, mm(KA, PmB));
+  M3 nBB = msub(PBB, mm(KB, PmB));
+  M3 I3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+  M3 nmm = mscale(r, msub(I3, mscale(r, Si)));
+  M3 nmA = mscale(r, mm(Si, PmA));
+  M3 nmB = mscale(r, mm(Si, PmB));
+  pset(P, MB, MB, nmm);
+  if (MB < A) pset(P, MB, A, nmA); else pset(P, A, MB, tr(nmA));
+  pset(P, MB, B, nmB);
+  pset(P, A, A, nAA); pset(P, A, B, nAB); pset(P, B, B, nBB);
+}
+
+// ---------------------------------------------------------------------------
+// Reward / observation
+// ---------------------------------------------------------------------------
+// compute_ingenuity_reward (tasks/ekf_lee_landed.py:692-723).
+OUZ_HD float reward(V3 p, V3 target, Q4 q, V3 w, float& dist) {
+  V3 d = target - p;
+  dist = sqrtf(dot(d, d));
+  float pos_r = 1.0f / (1.0f + dist * dist);
+  float ups_z = 2.0f * q.w * q.w - 1.0f + q.z * q.z * 2.0f;      // quat_axis(q, 2).z
+  float tilt = fabsf(1.0f - ups_z);
+  float up_r = 5.0f / (1.0f + tilt * tilt);
+  float spin = fabsf(w.z);
+  float spin_r = 1.0f / (1.0f + spin * spin);
+  return pos_r + pos_r * (up_r + spin_r);
+}
+
+// ---------------------------------------------------------------------------
+// Lumped rigid-body integrator (build-defined; PhysX is closed — DESIGN.md §3)
+// ---------------------------------------------------------------------------
+constexpr float kGravity = 9.81f;
+
+OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float mass, V3 I, float dt, int substeps,
+                      float wmax) {
+  const float h = dt / (float)substeps;
+  const float inv_m = 1.0f / mass;
+  for (int s = 0; s < substeps; ++s) {
+    M3 R = quat_to_mat(q);
+    V3 fw = mv(R, f_b);
+    v = v + h * v3(fw.x * inv_m, fw.y * inv_m, fw.z * inv_m - kGravity);
+    V3 wb = mtv(R, w);
+    V3 Iw = mul(I, wb);
+    V3 c = cross(wb, Iw);
+    V3 wdot = v3((tau_b.x - c.x) / I.x, (tau_b.y - c.y) / I.y, (tau_b.z - c.z) / I.z);
+    wb = wb + h * wdot;
+    w = mv(R, wb);
+    float n = norm(w);
+    if (n > wmax) w = (wmax / n) * w;
+    p = p + h * v;
+    n = norm(w);
+    float th = 0.5f * h * n;
+    float sc = (th < 1e-4f) ? 0.5f * h * (1.0f - th * th * (1.0f / 6.0f)) : sinf(th) / n;
+    Q4 dq{w.x * sc, w.y * sc, w.z * sc, cosf(th)};
+    q = quat_mul(dq, q);
+    float qi = 1.0f / sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q = Q4{q.x * qi, q.y * qi, q.z * qi, q.w * qi};
+  }
+}
+
+}  // namespace ouz

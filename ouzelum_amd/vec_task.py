@@ -1,0 +1,285 @@
+"""VecTask-compatible quadrotor environment running entirely in HIP kernels.
+
+Mirrors the reference's ``VecTask`` surface that the PPO/RPO learners consume
+(tasks/base/vec_task.py:61-406):
+
+* ``num_envs``, ``num_obs``, ``num_acts``, ``observation_space`` (Box(-inf, inf, (13,))),
+  ``action_space`` (Box(-1, 1, (4,))), ``obs_buf``/``rew_buf``/``reset_buf``/``timeout_buf``/
+  ``progress_buf``/``extras``;
+* ``reset() -> {"obs": (N,13)}`` that does not touch the simulation — the first
+  ``step`` resets every env because ``reset_buf`` starts at ones (vec_task.py:269-270,377-389);
+* ``step(a) -> ({"obs"}, rew_buf, reset_buf, {"time_outs"})`` with lazy resets:
+  envs done at step t are re-initialised at the start of step t+1 and the returned
+  obs of a done env is its terminal obs (ekf_lee_landed.py:312-315);
+* ``rew_buf``/``reset_buf`` are returned by reference and overwritten by the next
+  step, exactly as the reference does (vec_task.py:359); ``obs`` likewise.
+
+One ``step`` is ONE kernel launch (``ouz_step``) on the current HIP stream with
+no host synchronisation.  Buffers are torch tensors owned here; the C library
+only holds their device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .spaces import Box
+
+TASK_IDS = {"Ouzelum": L.TASK_OUZELUM, "LeeLanded": L.TASK_LEE_LANDED, "EKFLeeLanded": L.TASK_EKF_LEE_LANDED,
+            "QuadTracking": L.TASK_TRACKING, "QuadFault": L.TASK_FAULT, "QuadMixed": L.TASK_MIXED}
+POMDP_IDS = {None: -1, "none": L.POMDP_NONE, "flicker": L.POMDP_FLICKER, "random_noise": L.POMDP_NOISE,
+             "flickering_and_random_noise": L.POMDP_FLICKER_NOISE}
+
+
+def task_info(task: int) -> L.OuzTaskInfo:
+    info = L.OuzTaskInfo()
+    L.check(L.lib.ouz_task_info_get(int(task), info), "ouz_task_info_get")
+    return info
+
+
+class QuadVecTask:
+    """Vectorised x500 quadrotor env (one HIP kernel per step)."""
+
+    def __init__(self, task="LeeLanded", num_envs=4096, sim_device="cuda:0", rl_device=None, seed=0,
+                 env_id_offset=0, num_envs_total=None, pomdp=None, pomdp_prob=None, clip_obs=5.0,
+                 clip_actions=1.0, track_episodes=False, **overrides):
+        if isinstance(task, str):
+            if task not in TASK_IDS:
+                raise ValueError(f"unknown task {task!r}; one of {sorted(TASK_IDS)}")
+            self.task_name, self.task = task, TASK_IDS[task]
+        else:
+            self.task = int(task)
+            self.task_name = {v: k for k, v in TASK_IDS.items()}[self.task]
+        if pomdp not in POMDP_IDS:
+            raise ValueError("pomdp was not in ['flicker', 'random_noise', 'flickering_and_random_noise']!")
+        if clip_obs != 5.0 or clip_actions != 1.0:
+            raise ValueError("clipObservations=5 and clipActions=1 are fixed by the kernel (cfg/task/*.yaml)")
+        dev = torch.device(sim_device)
+        if dev.type != "cuda":
+            raise L.OuzelumError(f"sim_device {sim_device!r}: the quadrotor step runs only on a HIP device; "
+                                 "there is no CPU pipeline (the CPU restatement lives in oracle/ and is test-only)")
+        if not torch.cuda.is_available():
+            raise L.OuzelumError("no HIP device visible: QuadVecTask needs an MI355X")
+        self.device = dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
+        self.rl_device = torch.device(rl_device) if rl_device is not None else self.device
+        n = int(num_envs)
+        cfg = L.OuzConfig()
+        L.lib.ouz_default_config(cfg)
+        cfg.task = self.task
+        cfg.num_envs = n
+        cfg.env_id_offset = int(env_id_offset)
+        cfg.num_envs_total = int(num_envs_total or n)
+        cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        cfg.device = self.device.index
+        cfg.pomdp = POMDP_IDS[pomdp]
+        cfg.pomdp_prob = -1.0 if pomdp_prob is None else float(pomdp_prob)
+        cfg.track_episodes = 1 if track_episodes else 0
+        for k, v in overrides.items():
+            if not hasattr(cfg, k):
+                raise TypeError(f"unknown config field {k}")
+            setattr(cfg, k, v)
+        self.cfg = cfg
+        info = task_info(self.task)
+        self.max_episode_length = info.max_episode_length
+        self.uses_actions = bool(info.uses_actions)
+        self.dt = cfg.dt
+
+        # --- VecTask-shaped attributes (vec_task.py:90-105) ---
+        self.num_environments = n
+        self.num_agents = 1
+        self.num_observations = L.NUM_OBS
+        self.num_states = 0
+        self.num_actions = L.NUM_ACT
+        self.control_freq_inv = 1
+        self.clip_obs = 5.0
+        self.clip_actions = 1.0
+        self.obs_space = Box(np.ones(self.num_obs) * -np.inf, np.ones(self.num_obs) * np.inf)
+        self.state_space = Box(np.ones(0) * -np.inf, np.ones(0) * np.inf)
+        self.act_space = Box(np.ones(self.num_actions) * -1.0, np.ones(self.num_actions) * 1.0)
+
+        # --- buffers (owned here; allocate_buffers vec_task.py:254-277) ---
+        with torch.cuda.device(self.device):
+            self.fstate = torch.empty((L.F_COUNT, n), dtype=torch.float32, device=self.device)
+            self.istate = torch.empty((L.I_COUNT, n), dtype=torch.int32, device=self.device)
+            self.obs_buf = torch.empty((n, L.NUM_OBS), dtype=torch.float32, device=self.device)
+            self.rew_buf = torch.empty(n, dtype=torch.float32, device=self.device)
+            self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
+            self.timeout_buf = torch.empty(n, dtype=torch.bool, device=self.device)
+            self._zero_actions = torch.zeros((n, L.NUM_ACT), dtype=torch.float32, device=self.device)
+        self.states_buf = torch.zeros((n, 0), dtype=torch.float32, device=self.device)
+        self.extras = {}
+        self.obs_dict = {}
+
+        handle = ctypes.c_void_p()
+        L.check(L.lib.ouz_create(cfg, handle), "ouz_create")
+        self._env = handle
+        bufs = L.OuzBuffers(L.ptr(self.fstate), L.ptr(self.istate), L.ptr(self.obs_buf), L.ptr(self.rew_buf),
+                            L.ptr(self.reset_buf), L.ptr(self.timeout_buf))
+        L.check(L.lib.ouz_bind(self._env, bufs), "ouz_bind")
+        L.check(L.lib.ouz_init_state(self._env, self._stream()), "ouz_init_state")
+
+    # ------------------------------------------------------------------ util
+    def _stream(self):
+        return L.stream_ptr(self.device)
+
+    def __del__(self):
+        env = getattr(self, "_env", None)
+        if env is not None and env.value:
+            try:
+                torch.cuda.synchronize(self.device)
+            except Exception:  # noqa: BLE001
+                pass
+            L.lib.ouz_destroy(env)
+            self._env = None
+
+    # ------------------------------------------------------- VecTask surface
+    @property
+    def observation_space(self):
+        return self.obs_space
+
+    @property
+    def action_space(self):
+        return self.act_space
+
+    @property
+    def num_envs(self) -> int:
+        return self.num_environments
+
+    @property
+    def num_acts(self) -> int:
+        return self.num_actions
+
+    @property
+    def num_obs(self) -> int:
+        return self.num_observations
+
+    @property
+    def progress_buf(self):
+        """progress_buf (int32 SoA row; the reference keeps int64)."""
+        return self.istate[L.I_PROGRESS]
+
+    @property
+    def root_states(self):
+        """(N, 13) view [p, q_xyzw, v, w] of the SoA state (ekf_lee_landed.py:84)."""
+        return self.fstate[0:13].t()
+
+    @property
+    def target_root_positions(self):
+        return self.fstate[L.F_TARGET:L.F_TARGET + 3].t()
+
+    @property
+    def sim_step_count(self) -> int:
+        return int(L.lib.ouz_get_step(self._env))
+
+    def landings(self) -> int:
+        """Total landings over all finished episodes (ekf_lee_landed.py:319-331 'Landoa')."""
+        return int(self.istate[L.I_LANDINGS].sum().item())
+
+    def episode_stats(self, drain=True):
+        """(sum of returns, count) of episodes finished since the last drain, as a float64
+        device tensor [sum, count] — the quantity config E all-reduces over RCCL.
+        Needs ``track_episodes=True`` (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35)."""
+        if not self.cfg.track_episodes:
+            raise RuntimeError("create the env with track_episodes=True")
+        out = torch.stack([self.fstate[L.F_EP_SUM].double().sum(), self.istate[L.I_EP_CNT].double().sum()])
+        if drain:
+            self.fstate[L.F_EP_SUM].zero_()
+            self.istate[L.I_EP_CNT].zero_()
+        return out
+
+    def zero_actions(self):
+        return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)
+
+    def _actions_ptr(self, actions):
+        if actions is None:
+            return L.ptr(self._zero_actions)
+        if not isinstance(actions, torch.Tensor):
+            raise TypeError("actions must be a torch tensor")
+        if actions.shape != (self.num_envs, self.num_actions):
+            raise ValueError(f"actions shape {tuple(actions.shape)} != {(self.num_envs, self.num_actions)}")
+        if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        self._last_actions = actions   # keep alive until the kernel has read it
+        return L.ptr(actions)
+
+    def step(self, actions):
+        """VecTask.step (vec_task.py:313-359): clamp -> pre -> simulate -> post -> timeouts -> obs clamp."""
+        L.check(L.lib.ouz_step(self._env, self._actions_ptr(actions), self._stream()), "ouz_step")
+        self.extras["time_outs"] = self.timeout_buf
+        self.obs_dict["obs"] = self.obs_buf
+        return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
+
+    def rollout(self, action_ring, n_steps):
+        """``n_steps`` consecutive steps over a ring of pre-staged action batches (T, N, 4)
+        with one C call (the train_vec.py env-only loop without Python in between)."""
+        if action_ring is None:
+            L.check(L.lib.ouz_step_n(self._env, L.ptr(self._zero_actions), 1, int(n_steps), self._stream()),
+                    "ouz_step_n")
+            return
+        L.require_hip_tensor(action_ring, "action_ring")
+        if action_ring.dim() != 3 or action_ring.shape[1:] != (self.num_envs, self.num_actions):
+            raise ValueError("action_ring must be (T, num_envs, 4)")
+        L.check(L.lib.ouz_step_n(self._env, L.ptr(action_ring), action_ring.shape[0], int(n_steps),
+                                 self._stream()), "ouz_step_n")
+
+    def reset(self):
+        """vec_task.py:377-389: returns the current obs, does not touch the simulation."""
+        self.obs_dict["obs"] = self.obs_buf
+        return self.obs_dict
+
+    def reset_idx(self, env_ids):
+        """Mark envs for the lazy reset applied at the start of the next step."""
+        ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
+        L.check(L.lib.ouz_reset_idx(self._env, L.ptr(ids), ids.numel(), self._stream()), "ouz_reset_idx")
+        self._last_ids = ids
+
+    def reset_done(self):
+        """vec_task.py:391-406."""
+        done = self.reset_buf.nonzero(as_tuple=False).flatten()
+        self.obs_dict["obs"] = self.obs_buf
+        return self.obs_dict, done
+
+    # ----------------------------------------------------------- state I/O
+    def state_dict(self):
+        """Env-state checkpoint (the reference never checkpoints env state)."""
+        return {"fstate": self.fstate.clone(), "istate": self.istate.clone(), "obs": self.obs_buf.clone(),
+                "rew": self.rew_buf.clone(), "reset": self.reset_buf.clone(), "timeouts": self.timeout_buf.clone(),
+                "step": self.sim_step_count, "task": self.task, "num_envs": self.num_envs}
+
+    def load_state_dict(self, sd):
+        if sd["task"] != self.task or sd["num_envs"] != self.num_envs:
+            raise ValueError("checkpoint is for a different task / env count")
+        self.fstate.copy_(sd["fstate"])
+        self.istate.copy_(sd["istate"])
+        self.obs_buf.copy_(sd["obs"])
+        self.rew_buf.copy_(sd["rew"])
+        self.reset_buf.copy_(sd["reset"])
+        self.timeout_buf.copy_(sd["timeouts"])
+        L.check(L.lib.ouz_set_step(self._env, int(sd["step"])), "ouz_set_step")
+
+
+def make(seed: int, task: str, num_envs: int, sim_device: str = "cuda:0", rl_device: str = "cuda:0",
+         graphics_device_id: int = -1, headless: bool = False, multi_gpu: bool = False,
+         virtual_screen_capture: bool = False, force_render: bool = True, cfg=None, **kwargs):
+    """``isaacgymenvs.make`` signature (isaacgymenvs/__init__.py:14-55).
+
+    Unlike the reference (which ignores ``seed`` for the env, rlgames_utils.py:40-92),
+    ``seed`` keys the counter RNG.  With ``multi_gpu`` the process's LOCAL_RANK /
+    WORLD_SIZE shard the envs: this rank simulates global env ids
+    [rank*num_envs, (rank+1)*num_envs) on cuda:LOCAL_RANK.
+    """
+    import os
+    if cfg is not None:
+        kwargs = {**dict(cfg), **kwargs}
+    if multi_gpu:
+        rank = int(os.environ.get("RANK", os.environ.get("LOCAL_RANK", 0)))
+        local = int(os.environ.get("LOCAL_RANK", 0))
+        world = int(os.environ.get("WORLD_SIZE", 1))
+        sim_device = rl_device = f"cuda:{local}"
+        kwargs.setdefault("env_id_offset", rank * int(num_envs))
+        kwargs.setdefault("num_envs_total", world * int(num_envs))
+    return QuadVecTask(task=task, num_envs=num_envs, sim_device=sim_device, rl_device=rl_device, seed=seed, **kwargs)
+

@@ -1,0 +1,88 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol
+include/ouzelum.h declares, the Python mirror of its constants matches the
+header, and argument validation fails loudly (no GPU compute is called)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ouzelum.h")
+
+
+@pytest.fixture(scope="module")
+def L():
+    from ouzelum_amd import _lib
+    return _lib
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(ouz_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol(L):
+    names = header_functions()
+    assert len(names) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (ouz_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    assert set(names) == set(L.SIGNATURES), "ctypes SIGNATURES table must list exactly the header's functions"
+    for n in names:
+        assert hasattr(L.lib, n)
+
+
+def test_header_constants_match_python_mirror(L):
+    src = open(HEADER).read()
+    defines = dict(re.findall(r"#define (OUZ_\w+) \(?(-?\d+)\)?", src))
+    assert int(defines["OUZ_ABI_VERSION"]) == L.ABI_VERSION == L.lib.ouz_abi_version()
+    assert int(defines["OUZ_TASK_MIXED"]) == L.TASK_MIXED and int(defines["OUZ_NUM_TASKS"]) == L.NUM_TASKS
+    assert int(defines["OUZ_POMDP_FLICKER_NOISE"]) == L.POMDP_FLICKER_NOISE
+    enums = dict(re.findall(r"(OUZ_[FI]_\w+) = (\d+)", src))
+    for k, v in enums.items():
+        assert getattr(L, k[4:]) == int(v), k
+
+
+def test_struct_layout(L):
+    # must equal the static_asserts in quad_kernels.hip
+    assert ctypes.sizeof(L.OuzConfig) == 88
+    assert ctypes.sizeof(L.OuzBuffers) == 48
+
+
+def test_argument_validation_without_gpu(L):
+    cfg = L.OuzConfig()
+    L.lib.ouz_default_config(cfg)
+    assert cfg.dt == pytest.approx(0.01) and cfg.substeps == 2 and cfg.convergence_time == 300
+    h = ctypes.c_void_p()
+    bad = L.OuzConfig.from_buffer_copy(cfg)
+    bad.task = 17
+    assert L.lib.ouz_create(bad, h) == -1 and b"unknown task" in L.lib.ouz_last_error()
+    bad = L.OuzConfig.from_buffer_copy(cfg)
+    bad.num_envs = 0
+    assert L.lib.ouz_create(bad, h) == -1
+    bad = L.OuzConfig.from_buffer_copy(cfg)
+    bad.env_id_offset, bad.num_envs_total = 4096, 4096
+    assert L.lib.ouz_create(bad, h) == -1 and b"out of range" in L.lib.ouz_last_error()
+    assert L.lib.ouz_step(None, None, None) == -3
+    assert L.lib.ouz_lee_control(0, None, None, None, None, 0, None) == 0          # n == 0 is a no-op
+    assert L.lib.ouz_lee_control(5, None, None, None, None, 4, None) == -1
+    with pytest.raises(ValueError):
+        L.check(-1, "x")
+
+
+def test_task_info(L):
+    import ouzelum_amd as o
+    assert o.task_info(L.TASK_EKF_LEE_LANDED).max_episode_length == 700       # EKFLeeLanded.yaml:10
+    assert o.task_info(L.TASK_OUZELUM).max_episode_length == 2000             # Ouzelum.yaml:10
+    assert o.task_info(L.TASK_OUZELUM).z_die == pytest.approx(0.5)            # ouzelum.py:327
+    assert o.task_info(L.TASK_LEE_LANDED).uses_actions == 0
+
+
+def test_no_cpu_fallback():
+    import ouzelum_amd as o
+    from ouzelum_amd._lib import OuzelumError
+    with pytest.raises(OuzelumError):
+        o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="cpu", rl_device="cpu")

@@ -1,0 +1,78 @@
+"""Pin the CPU oracle against golden vectors produced by the reference's own modules.
+
+Fixtures: tests/golden/*.npz, written by tests/golden/make_golden.py from
+isaacgymenvs/controllers/*, ahrs_ekf.py, PVFilter.py, utils/trajectories.py and
+poselib rotation3d.quat_rotate (see that script's header for what was stubbed).
+"""
+import numpy as np
+import pytest
+
+from oracle import quad_oracle as Q
+
+MODES = {"lee_position_control": Q.LEE_POSITION, "lee_velocity_control": Q.LEE_VELOCITY,
+         "lee_attitude_control": Q.LEE_ATTITUDE}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_lee_vs_reference(golden, mode, seed):
+    g = golden("lee_controllers.npz")
+    k = f"{mode}_s{seed}_f64"
+    T, tau = Q.controller(MODES[mode], g[k + "_state"].copy(), g[k + "_cmd"].copy())
+    # reference f64 run with f32 gain tensors promoted -> agree to ~1e-7 relative of the gains
+    np.testing.assert_allclose(T, g[k + "_thrust"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(tau, g[k + "_torque"], rtol=1e-6, atol=1e-6)
+    # the reference's own f32 run agrees within f32 round-off
+    k32 = f"{mode}_s{seed}_f32"
+    T32, tau32 = Q.controller(MODES[mode], g[k32 + "_state"].astype(np.float64), g[k32 + "_cmd"].astype(np.float64))
+    np.testing.assert_allclose(T32, g[k32 + "_thrust"], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(tau32, g[k32 + "_torque"], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_ekf_vs_reference(golden, seed):
+    g = golden("ekf.npz")
+    dt = float(g["dt"])
+    q = g[f"s{seed}_q0"].copy()
+    P = np.broadcast_to(np.eye(4), (q.shape[0], 4, 4)).copy()
+    for t in range(g[f"s{seed}_gyr"].shape[0]):
+        qn = q / np.linalg.norm(q, axis=1, keepdims=True)
+        q, P = Q.ekf_update(qn, P, g[f"s{seed}_gyr"][t], g[f"s{seed}_ang"][t], Dt=dt)
+        np.testing.assert_allclose(q, g[f"s{seed}_q"][t], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(P, g[f"s{seed}_P"][t], rtol=1e-7, atol=1e-18)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pvfilter_vs_reference(golden, seed):
+    g = golden("pvfilter.npz")
+    dt = float(g["dt"])
+    x = g[f"s{seed}_x0"].copy()
+    n = x.shape[0]
+    P = np.broadcast_to(np.eye(9) * Q.PV_P0, (n, 9, 9)).copy()
+    T = g[f"s{seed}_acc"].shape[0]
+    for t in range(T):
+        x, P = Q.pv_predict(x, P, g[f"s{seed}_acc"][t], g[f"s{seed}_q_wxyz"][t], dt=dt)
+        # shared-counter trigger pattern (ekf_lee_landed.py:425-440) in closed form
+        gidx = t * n + np.arange(n)
+        tp, tv = (gidx % 7) == 6, (gidx % 3) == 0
+        np.testing.assert_array_equal(tp, g[f"s{seed}_trig_p"][t])
+        np.testing.assert_array_equal(tv, g[f"s{seed}_trig_v"][t])
+        if tp.any():
+            x[tp], P[tp] = Q.pv_correct(x[tp], P[tp], g[f"s{seed}_pos"][t][tp], 0, Q.PV_POS_VAR)
+        if tv.any():
+            x[tv], P[tv] = Q.pv_correct(x[tv], P[tv], g[f"s{seed}_vel"][t][tv], 1, 0.0)
+        # The filter amplifies f64 round-off by its conditioning (P0 = 1000 against
+        # R = 1e-7, i.e. ~1e10): two f64 evaluations in different operation order
+        # agree only to ~3e-7 of the state's magnitude.  Norm-wise tolerance:
+        gx, gP = g[f"s{seed}_x"][t], g[f"s{seed}_P"][t]
+        assert np.abs(x - gx).max() <= 1e-6 * np.abs(gx).max()
+        assert np.abs(P - gP).max() <= 1e-7 * np.abs(gP).max()
+
+
+def test_trajectories_and_quat_rotate(golden):
+    g = golden("traj_quat.npz")
+    lem, cir, sq = Q.waypoint_tables()
+    np.testing.assert_allclose(lem, g["lemniscate"], atol=1e-6)
+    np.testing.assert_allclose(cir, g["circle"], atol=1e-6)
+    np.testing.assert_array_equal(sq, g["square"])
+    np.testing.assert_allclose(Q.quat_rotate_xyzw(g["quat_xyzw"], g["vec"]), g["quat_rotate"], atol=1e-12)
