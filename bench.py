@@ -82,23 +82,24 @@ def action_ring(n, dev, seed):
 
 
 def kernel_time_us(env, ring, reps=200):
-    """Average duration of one step kernel from HIP events bracketing each launch on the
-    stream the kernel runs on.  The stream is first held by a spin kernel so every
-    (event, kernel, event) triple is queued before the GPU reaches it and no host
-    launch gap lands inside a bracket."""
+    """Average duration of one step kernel from HIP events on the stream the kernel runs on.
+
+    The stream is first held by a spin kernel so that all ``reps`` launches (one
+    ``ouz_step_n`` C loop) are queued before the GPU reaches them; the bracket then
+    holds ``reps`` back-to-back kernels and no host launch gap, i.e. kernel time plus
+    the ~1 us dependent-launch boundary (MI355X_MICROARCH.md 'boundary' row)."""
     dev = env.device
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize(dev)
     try:
-        torch.cuda._sleep(int(3e7))
+        torch.cuda._sleep(int(2e7))
     except Exception:  # noqa: BLE001
         pass
-    for s, e in evs:
-        s.record()
-        env.rollout(ring, 1)
-        e.record()
+    s.record()
+    env.rollout(ring, reps)
+    e.record()
     torch.cuda.synchronize(dev)
-    return float(np.mean([s.elapsed_time(e) for s, e in evs])) * 1e3
+    return s.elapsed_time(e) * 1e3 / reps
 
 
 def roofline_entry(task, n, us, track=True):
