@@ -38,17 +38,17 @@ RING = 16
 # Algorithmic bytes per env-step of quad_step_kernel<TASK>: every
 # field the kernel must read and write per env, SoA f32 / i32, obs AoS f32,
 # reset i64, timeouts u8.  Reset-only and done-only traffic is excluded.
+_CORE = 8 + 52 + 4 + 52 + 4 + 52 + 4 + 8 + 1   # reset r, p/q/v/w r+w, progress r+w, obs w, rew w, reset w, timeouts w
 BYTES_PER_ENV_STEP = {
-    # reset(8) p,q,v,w(52) progress(4) land_flag(4) r | p,q,v,w(52) progress(4) land_flag(4) obs(52) rew(4) reset(8) timeouts(1) w
-    "LeeLanded": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1,
-    # + target(12 r/w) + thrust(16 r/w) + actions(16 r)
-    "Ouzelum": 8 + 52 + 4 + 4 + 12 + 16 + 16 + 52 + 4 + 4 + 12 + 16 + 52 + 4 + 8 + 1,
-    # Ouzelum + fault rotor/onset/eta (12 r)
-    "QuadFault": 8 + 52 + 4 + 4 + 12 + 16 + 16 + 12 + 52 + 4 + 4 + 12 + 16 + 52 + 4 + 8 + 1,
-    # LeeLanded + prev_v(12) ekf q,P(56) pv x,P(216) waypoint(12), each r/w
-    "EKFLeeLanded": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1 + 2 * (12 + 56 + 216 + 12),
-    # EKF + dr(12 r) + platform(8 r/w) + traj type/idx/sd (12 r, 4 w)
-    "QuadTracking": 8 + 52 + 4 + 4 + 52 + 4 + 4 + 52 + 4 + 8 + 1 + 2 * (12 + 56 + 216 + 12) + 12 + 16 + 12 + 4,
+    "LeeLanded": _CORE,
+    # + random-goal target (12 r/w), rotor thrusts (16 r/w), actions (16 r)
+    "Ouzelum": _CORE + 2 * 12 + 2 * 16 + 16,
+    # + fault rotor / onset / eta (12 r)
+    "QuadFault": _CORE + 2 * 12 + 2 * 16 + 16 + 12,
+    # + prev_v (12), EKF q + packed P (56), PV x + packed P (216), waypoint (12), each r/w
+    "EKFLeeLanded": _CORE + 2 * (12 + 56 + 216 + 12),
+    # + DR scales (12 r), platform xy (8 r/w), trajectory type / index / scale (12 r, 4 w)
+    "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 16 + 12 + 4,
 }
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0

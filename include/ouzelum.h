@@ -144,6 +144,8 @@ typedef struct ouz_task_info {
   int32_t pomdp;
   float pomdp_prob;
   int32_t uses_actions;     /* 1 for RL-thrust tasks; Lee tasks ignore actions (ekf_lee_landed.py:308) */
+  int32_t target_mode;      /* 0 random goal (stored), 1 fixed platform, 2 trajectory platform       */
+  float plat_offset_x;      /* target x = platform x + offset (lee_landed.py:629, ekf_lee_landed.py:629) */
 } ouz_task_info;
 
 typedef struct ouz_env ouz_env;

@@ -27,6 +27,9 @@ NUM_TASKS = 6
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
 LEE_POSITION, LEE_VELOCITY, LEE_ATTITUDE = range(3)
 NUM_OBS, NUM_ACT = 13, 4
+TGT_GOAL, TGT_PLATFORM, TGT_TRAJ = range(3)
+MIXED_CHUNK = 64
+MIXED_TASKS = (TASK_LEE_LANDED, TASK_TRACKING, TASK_FAULT)
 F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
 F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
 F_EP_RET, F_EP_SUM = 101, 102
@@ -53,7 +56,8 @@ class OuzBuffers(ctypes.Structure):
 
 class OuzTaskInfo(ctypes.Structure):
     _fields_ = [("max_episode_length", ctypes.c_int32), ("z_die", ctypes.c_float), ("land_radius", ctypes.c_float),
-                ("pomdp", ctypes.c_int32), ("pomdp_prob", ctypes.c_float), ("uses_actions", ctypes.c_int32)]
+                ("pomdp", ctypes.c_int32), ("pomdp_prob", ctypes.c_float), ("uses_actions", ctypes.c_int32),
+                ("target_mode", ctypes.c_int32), ("plat_offset_x", ctypes.c_float)]
 
 
 _P = ctypes.c_void_p

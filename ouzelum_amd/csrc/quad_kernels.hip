@@ -63,6 +63,7 @@ struct EnvConsts {
   float dt, thrust_step, thrust_max, plat_speed, dr_lo, dr_hi, fault_eta_hi, wmax;
   int32_t substeps, conv_time;
   float mass, ixx, iyy, izz;
+  float inv_mass, inv_ixx, inv_iyy, inv_izz;
 };
 
 struct StepArgs {
@@ -150,7 +151,7 @@ __device__ __forceinline__ float2 traj_point(const StepArgs& a, int type, int id
 // The fused step for one env (mirrors oracle/quad_oracle.py::OracleEnv.step)
 // ---------------------------------------------------------------------------
 template <int CTRL, int TGT>
-__device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid, int task) {
+__device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid, int task, float* ob) {
   const TaskParams& tp = a.tp[task];
   const EnvConsts& c = a.c;
   const bool rst = a.reset[i] != 0;
@@ -159,8 +160,13 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
   V3 v = ld3(a, OUZ_F_V, i);
   V3 w = ld3(a, OUZ_F_W, i);
   int32_t progress = ldi(a, OUZ_I_PROGRESS, i);
-  int32_t land_flag = ldi(a, OUZ_I_LAND_FLAG, i);
-  V3 target = ld3(a, OUZ_F_TARGET, i);
+  // target_root_positions: random goals are state (ouzelum.py:180-190); a platform target is
+  // platform xy + offset at z 0.377 (ekf_lee_landed.py:87,628-629) and is recomputed, not stored.
+  // Before the first post_physics_step it is still (0, 0, 0.377).
+  V3 target;
+  if constexpr (TGT == TGT_GOAL) target = ld3(a, OUZ_F_TARGET, i);
+  else target = v3(a.step == 0 ? 0.0f : tp.plat_off_x, 0.0f, 0.377f);
+  float2 plat = make_float2(0.0f, 0.0f);
   float dr_m = 1.0f, dr_i = 1.0f, dr_t = 1.0f;
   if (tp.dr) { dr_m = ld(a, OUZ_F_DR, i); dr_i = ld(a, OUZ_F_DR + 1, i); dr_t = ld(a, OUZ_F_DR + 2, i); }
 
@@ -172,8 +178,11 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
     v = v3(0.0f, 0.0f, 0.0f);
     w = v3(0.0f, 0.0f, 0.0f);
     progress = 0;
-    sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + land_flag);
-    land_flag = 0;
+    const int32_t lf = ldi(a, OUZ_I_LAND_FLAG, i);     // landing counter (ekf_lee_landed.py:323-331)
+    if (lf) {
+      sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + lf);
+      sti(a, OUZ_I_LAND_FLAG, i, 0);
+    }
     if (tp.dr) {
       U4 d = draw(a.seed, gid, a.step, RNG_DR);
       dr_m = uniform_f32(d.x, c.dr_lo, c.dr_hi);
@@ -231,7 +240,11 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
     lee_position(p, q, v, w, cmd, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
     V3 dd = cmd - p;
-    if (sqrtf(dot(dd, dd)) < tp.land_radius) { land_flag = 1; fz = 0.0f; tau = v3(0.0f, 0.0f, 0.0f); }
+    if (sqrtf(dot(dd, dd)) < tp.land_radius) {
+      sti(a, OUZ_I_LAND_FLAG, i, 1);
+      fz = 0.0f;
+      tau = v3(0.0f, 0.0f, 0.0f);
+    }
     if (rst) fz = 0.0f;                        // forces[reset] = 0, torques kept
     f_b = v3(0.0f, 0.0f, fz * dr_t);
     tau_b = tau;
@@ -243,6 +256,7 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
       int ttype = ldi(a, OUZ_I_TRAJ_TYPE, i), tidx = ldi(a, OUZ_I_TRAJ_IDX, i);
       float sd = ld(a, OUZ_F_TRAJ_SD, i);
       float2 pl = make_float2(ld(a, OUZ_F_PLAT, i), ld(a, OUZ_F_PLAT + 1, i));
+      if (a.step != 0) { target.x = pl.x + tp.plat_off_x; target.y = pl.y; }
       float2 wpp = traj_point(a, ttype, tidx, sd);
       float dx = wpp.x - pl.x, dy = wpp.y - pl.y;
       if (sqrtf(dx * dx + dy * dy) < 0.2f) tidx += 1;
@@ -264,6 +278,7 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
         pl.x += dx * s; pl.y += dy * s;
       }
       st(a, OUZ_F_PLAT, i, pl.x); st(a, OUZ_F_PLAT + 1, i, pl.y);
+      plat = pl;
     }
     V3 prev_v = ld3(a, OUZ_F_PREV_V, i);
     V3 lin_acc = v3((v.x - prev_v.x) / c.dt, (v.y - prev_v.y) / c.dt, (v.z - prev_v.z) / c.dt);
@@ -334,7 +349,7 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
     else lee_position(v3(px[0], px[1], px[2]), q, v3(px[3], px[4], px[5]), w, wp, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
     if (td < tp.land_radius) {                       // :508-515
-      if (!conv) land_flag = 1;
+      if (!conv) sti(a, OUZ_I_LAND_FLAG, i, 1);
       fz = 0.0f;
       tau = v3(0.0f, 0.0f, 0.0f);
     }
@@ -345,19 +360,26 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
   }
 
   // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
-  integrate(p, q, v, w, f_b, tau_b, c.mass * dr_m, v3(c.ixx * dr_i, c.iyy * dr_i, c.izz * dr_i), c.dt, c.substeps, c.wmax);
+  {
+    const V3 I = v3(c.ixx * dr_i, c.iyy * dr_i, c.izz * dr_i);
+    const float inv_m = tp.dr ? 1.0f / (c.mass * dr_m) : c.inv_mass;
+    const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
+    integrate(p, q, v, w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax);
+  }
 
   // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
   progress += 1;
   if constexpr (TGT == TGT_PLATFORM || TGT == TGT_TRAJ) {
-    float plx = 0.0f, ply = 0.0f;
-    if constexpr (TGT == TGT_TRAJ) { plx = ld(a, OUZ_F_PLAT, i); ply = ld(a, OUZ_F_PLAT + 1, i); }
-    target.x = plx + tp.plat_off_x;
-    target.y = ply;
+    target.x = plat.x + tp.plat_off_x;
+    target.y = plat.y;
   }
-  float ob[13] = {(target.x - p.x) / 3.0f, (target.y - p.y) / 3.0f, (target.z - p.z) / 3.0f, q.x, q.y, q.z, q.w,
-                  v.x / 2.0f, v.y / 2.0f, v.z / 2.0f, w.x / kPiF, w.y / kPiF, w.z / kPiF};
+  ob[0] = (target.x - p.x) / 3.0f; ob[1] = (target.y - p.y) / 3.0f; ob[2] = (target.z - p.z) / 3.0f;
+  ob[3] = q.x; ob[4] = q.y; ob[5] = q.z; ob[6] = q.w;
+  ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
+  ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
   pomdp_apply<13>(ob, tp, task, a, gid, SITE_OBS, false);
+#pragma unroll
+  for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
   float r = reward(p, target, q, w, dist);
   const bool timeout_len = progress >= tp.max_ep - 1;
@@ -369,12 +391,8 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
   st(a, OUZ_F_Q, i, q.x); st(a, OUZ_F_Q + 1, i, q.y); st(a, OUZ_F_Q + 2, i, q.z); st(a, OUZ_F_Q + 3, i, q.w);
   st3(a, OUZ_F_V, i, v);
   st3(a, OUZ_F_W, i, w);
-  st3(a, OUZ_F_TARGET, i, target);
+  if constexpr (TGT == TGT_GOAL) st3(a, OUZ_F_TARGET, i, target);
   sti(a, OUZ_I_PROGRESS, i, progress);
-  sti(a, OUZ_I_LAND_FLAG, i, land_flag);
-  float* o = a.obs + (size_t)i * OUZ_NUM_OBS;
-#pragma unroll
-  for (int k = 0; k < 13; ++k) o[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   a.rew[i] = r;
   if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
     float er = ld(a, OUZ_F_EP_RET, i) + r;
@@ -389,25 +407,45 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
   a.timeouts[i] = (timeout_len && rs) ? 1 : 0;                             // vec_task.py:345
 }
 
+constexpr int kMaxBlock = 256;
+
 template <int TASK>
-__global__ void __launch_bounds__(256) quad_step_kernel(StepArgs a) {
+__global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a) {
+  // obs is (N, 13) AoS for the learners (vec_task.py:254-258).  A lane's 13 floats are staged
+  // through LDS (stride 13 dwords: conflict-free) and the block writes its contiguous
+  // 52*blockDim-byte slice with 16-byte stores instead of 13 strided dword stores per lane.
+  __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
+  float* s_obs = reinterpret_cast<float*>(s_obs4);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const uint32_t gid = a.env_offset + (uint32_t)i;
-  if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-    env_step<CTRL_RL, TGT_GOAL>(a, i, gid, TASK);
-  } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-    env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, TASK);
-  } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-    env_step<CTRL_LEE_EST, TGT_PLATFORM>(a, i, gid, TASK);
-  } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-    env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, TASK);
-  } else {
-    const int t = mixed_task(gid);   // wave-uniform: 64-env blocks
-    if (t == OUZ_TASK_LEE_LANDED) env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, t);
-    else if (t == OUZ_TASK_TRACKING) env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, t);
-    else env_step<CTRL_RL, TGT_GOAL>(a, i, gid, t);
+  const bool valid = i < a.n;
+  float ob[OUZ_NUM_OBS];
+  if (valid) {
+    const uint32_t gid = a.env_offset + (uint32_t)i;
+    if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
+      env_step<CTRL_RL, TGT_GOAL>(a, i, gid, TASK, ob);
+    } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
+      env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, TASK, ob);
+    } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
+      env_step<CTRL_LEE_EST, TGT_PLATFORM>(a, i, gid, TASK, ob);
+    } else if constexpr (TASK == OUZ_TASK_TRACKING) {
+      env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, TASK, ob);
+    } else {
+      const int t = mixed_task(gid);   // wave-uniform: 64-env blocks
+      if (t == OUZ_TASK_LEE_LANDED) env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, t, ob);
+      else if (t == OUZ_TASK_TRACKING) env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, t, ob);
+      else env_step<CTRL_RL, TGT_GOAL>(a, i, gid, t, ob);
+    }
+#pragma unroll
+    for (int k = 0; k < OUZ_NUM_OBS; ++k) s_obs[threadIdx.x * OUZ_NUM_OBS + k] = ob[k];
   }
+  __syncthreads();
+  const int base = blockIdx.x * blockDim.x;
+  const int nvalid = min((int)blockDim.x, a.n - base);
+  const int nf = nvalid * OUZ_NUM_OBS;            // floats of this block's slice
+  float* dst = a.obs + (size_t)base * OUZ_NUM_OBS; // 16-B aligned: blockDim is a multiple of 64
+  float4* dst4 = reinterpret_cast<float4*>(dst);
+  for (int k = threadIdx.x; k < nf / 4; k += blockDim.x) dst4[k] = s_obs4[k];
+  for (int k = (nf / 4) * 4 + threadIdx.x; k < nf; k += blockDim.x) dst[k] = s_obs[k];
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
@@ -514,8 +552,9 @@ __global__ void integrate_kernel(float* root, const float* fb, const float* tb, 
   float* s = root + (size_t)i * 13;
   V3 p = v3(s[0], s[1], s[2]), v = v3(s[7], s[8], s[9]), w = v3(s[10], s[11], s[12]);
   Q4 q{s[3], s[4], s[5], s[6]};
-  integrate(p, q, v, w, v3(fb[i * 3], fb[i * 3 + 1], fb[i * 3 + 2]), v3(tb[i * 3], tb[i * 3 + 1], tb[i * 3 + 2]), mass[i],
-            v3(inertia[i * 3], inertia[i * 3 + 1], inertia[i * 3 + 2]), dt, substeps, 4.0f * kPiF);
+  const V3 I = v3(inertia[i * 3], inertia[i * 3 + 1], inertia[i * 3 + 2]);
+  integrate(p, q, v, w, v3(fb[i * 3], fb[i * 3 + 1], fb[i * 3 + 2]), v3(tb[i * 3], tb[i * 3 + 1], tb[i * 3 + 2]),
+            1.0f / mass[i], I, v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z), dt, substeps, 4.0f * kPiF);
   s[0] = p.x; s[1] = p.y; s[2] = p.z; s[3] = q.x; s[4] = q.y; s[5] = q.z; s[6] = q.w;
   s[7] = v.x; s[8] = v.y; s[9] = v.z; s[10] = w.x; s[11] = w.y; s[12] = w.z;
 }
@@ -549,7 +588,7 @@ using namespace ouz;
 
 static_assert(sizeof(ouz_config) == 88, "ctypes OuzConfig mirror (ouzelum_amd/_lib.py)");
 static_assert(sizeof(ouz_buffers) == 48, "ctypes OuzBuffers mirror");
-static_assert(sizeof(ouz_task_info) == 24, "ctypes OuzTaskInfo mirror");
+static_assert(sizeof(ouz_task_info) == 32, "ctypes OuzTaskInfo mirror");
 
 namespace {
 thread_local std::string g_err;
@@ -606,11 +645,12 @@ void ouz_default_config(ouz_config* c) {
 int ouz_task_info_get(int32_t task, ouz_task_info* out) {
   if (!out || task < 0 || task >= OUZ_NUM_TASKS) return fail(OUZ_ERR_INVALID, "ouz_task_info_get: bad task");
   if (task == OUZ_TASK_MIXED) {
-    *out = ouz_task_info{2000, 0.3f, 0.2f, -1, -1.0f, 1};
+    *out = ouz_task_info{2000, 0.3f, 0.2f, -1, -1.0f, 1, -1, 0.0f};
     return OUZ_OK;
   }
   TaskParams t = task_preset(task);
-  *out = ouz_task_info{t.max_ep, t.z_die, t.land_radius, t.pomdp, t.pomdp_prob, t.ctrl == CTRL_RL ? 1 : 0};
+  *out = ouz_task_info{t.max_ep, t.z_die, t.land_radius, t.pomdp, t.pomdp_prob, t.ctrl == CTRL_RL ? 1 : 0,
+                       t.target_mode, t.plat_off_x};
   return OUZ_OK;
 }
 
@@ -675,7 +715,8 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   }
   a.c = EnvConsts{cfg->dt, (float)((double)cfg->dt * (double)cfg->thrust_rate), cfg->thrust_max, cfg->plat_speed,
                   cfg->dr_lo, cfg->dr_hi, cfg->fault_eta_hi, (float)(4.0 * 3.14159265358979323846),
-                  cfg->substeps, cfg->convergence_time, (float)mass, (float)ixx, (float)ixx, (float)izz};
+                  cfg->substeps, cfg->convergence_time, (float)mass, (float)ixx, (float)ixx, (float)izz,
+                  1.0f / (float)mass, 1.0f / (float)ixx, 1.0f / (float)ixx, 1.0f / (float)izz};
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
     TaskParams tp = task_preset(t);
     if (cfg->pomdp >= 0) tp.pomdp = cfg->pomdp;

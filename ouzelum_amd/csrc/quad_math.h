@@ -100,18 +100,44 @@ OUZ_HD M3 quat_to_mat(Q4 q) {
              two_s * (i * k - j * r), two_s * (j * k + i * r), 1.0f - two_s * (i * i + j * j)}};
 }
 
-// matrix_to_euler_angles(R, "ZYX")[:, [2,1,0]] (rotation_conversions.py:216-255).
+// matrix_to_euler_angles(R, "ZYX")[:, [2,1,0]] (rotation_conversions.py:216-255):
+// roll = atan2(R21, R22), pitch = asin(-R20), yaw = atan2(R10, R00).
+// The controllers only consume sin/cos of these angles (position_control.py:51-52,75-79),
+// so they are formed directly from R: cos(atan2(y, x)) = x / hypot(x, y), etc. — the
+// same numbers without 2 atan2 + 1 asin + 6 sin/cos per env.  Only the position
+// controller needs the yaw angle itself (its yaw-rate error, :89-92).
+struct EulerSC { float sr, cr, sp, cp, sy, cy; };
+
+OUZ_HD void unit2(float y, float x, float& s, float& c) {
+  float h2 = x * x + y * y;
+  if (h2 > 0.0f) { float ih = 1.0f / sqrtf(h2); s = y * ih; c = x * ih; }
+  else { s = 0.0f; c = 1.0f; }     // atan2(0, 0) = 0
+}
+
+OUZ_HD EulerSC euler_sc(const M3& R) {
+  EulerSC e;
+  unit2(R.m[7], R.m[8], e.sr, e.cr);
+  e.sp = -R.m[6];
+  e.cp = sqrtf(fmaxf(0.0f, 1.0f - R.m[6] * R.m[6]));   // cos(asin(x)) >= 0
+  unit2(R.m[3], R.m[0], e.sy, e.cy);
+  return e;
+}
+
 OUZ_HD void mat_to_rpy(const M3& R, float& roll, float& pitch, float& yaw) {
   roll = atan2f(R.m[7], R.m[8]);
   pitch = asinf(-R.m[6]);
   yaw = atan2f(R.m[3], R.m[0]);
 }
 
-// euler_angles_to_matrix((yaw, pitch, roll), "ZYX") = Rz Ry Rx (rotation_conversions.py:149-171).
-OUZ_HD M3 rpy_to_mat(float yaw, float pitch, float roll) {
-  float cz = cosf(yaw), sz = sinf(yaw), cy = cosf(pitch), sy = sinf(pitch), cx = cosf(roll), sx = sinf(roll);
+// euler_angles_to_matrix((yaw, pitch, roll), "ZYX") = Rz Ry Rx from sines/cosines.
+OUZ_HD M3 rpy_to_mat_sc(float cz, float sz, float cy, float sy, float cx, float sx) {
   return M3{{cz * cy, cz * sy * sx - sz * cx, cz * sy * cx + sz * sx, sz * cy, sz * sy * sx + cz * cx,
              sz * sy * cx - cz * sx, -sy, cy * sx, cy * cx}};
+}
+
+// euler_angles_to_matrix((yaw, pitch, roll), "ZYX") = Rz Ry Rx (rotation_conversions.py:149-171).
+OUZ_HD M3 rpy_to_mat(float yaw, float pitch, float roll) {
+  return rpy_to_mat_sc(cosf(yaw), sinf(yaw), cosf(pitch), sinf(pitch), cosf(roll), sinf(roll));
 }
 
 // my_quat_rotate / quat_rotate, xyzw (utils/torch_jit_utils.py:198-208).
@@ -148,7 +174,7 @@ OUZ_HD float remainder_f(float a, float b) {
 }
 
 // Shared attitude loop (position_control.py:66-108): returns torque.
-OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, float roll, float pitch, float yaw_rate,
+OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, const EulerSC& e, float yaw_rate,
                             const LeeGains& g) {
   // A = Rd^T R ; vee(A - A^T) = (A21 - A12, A02 - A20, A10 - A01)
   M3 A;
@@ -158,8 +184,8 @@ OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, float roll, flo
     for (int j = 0; j < 3; ++j)
       A.m[i * 3 + j] = Rd.m[0 * 3 + i] * R.m[0 * 3 + j] + Rd.m[1 * 3 + i] * R.m[1 * 3 + j] + Rd.m[2 * 3 + i] * R.m[2 * 3 + j];
   V3 e_R = v3(0.5f * (A.m[7] - A.m[5]), 0.5f * (A.m[2] - A.m[6]), 0.5f * (A.m[3] - A.m[1]));
-  float sp = sinf(pitch), cp = cosf(pitch), sr = sinf(roll), cr = cosf(roll);
-  V3 wd = v3(-sp * yaw_rate, sr * cp * yaw_rate, cr * cp * yaw_rate);
+  // omega_d = E (0, 0, yaw_rate), E = rotmat_euler_to_body_rates (:73-86)
+  V3 wd = v3(-e.sp * yaw_rate, e.sr * e.cp * yaw_rate, e.cr * e.cp * yaw_rate);
   V3 des = mtv(R, mv(Rd, wd));
   V3 act = mtv(R, omega);
   V3 e_w = act - des;
@@ -172,49 +198,45 @@ OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, float roll, flo
 OUZ_HD void lee_position(V3 p, Q4 q, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const LeeGains& g, float& thrust,
                          V3& torque) {
   M3 R = quat_to_mat(q);
-  float roll, pitch, yaw;
-  mat_to_rpy(R, roll, pitch, yaw);
+  EulerSC e = euler_sc(R);
   V3 a = mul(g.kP, cmd_p - p) - mul(g.kV, v);
   a.z += 1.0f;
   thrust = a.x * R.m[2] + a.y * R.m[5] + a.z * R.m[8];
-  float na = norm(a);
-  V3 b3 = v3(a.x / na, a.y / na, a.z / na);
-  V3 c = v3(cosf(yaw), sinf(yaw), 0.0f);
-  V3 b2 = cross(b3, c);
-  float nb = norm(b2);
-  b2 = v3(b2.x / nb, b2.y / nb, b2.z / nb);
+  V3 b3 = (1.0f / norm(a)) * a;
+  V3 b2 = cross(b3, v3(e.cy, e.sy, 0.0f));
+  b2 = (1.0f / norm(b2)) * b2;
   V3 b1 = cross(b2, b3);
   M3 Rd{{b1.x, b2.x, b3.x, b1.y, b2.y, b3.y, b1.z, b2.z, b3.z}};
-  float yr = remainder_f(cmd_yaw - yaw, kTwoPiF);
+  float yr = remainder_f(cmd_yaw - atan2f(R.m[3], R.m[0]), kTwoPiF);
   if (yr > kPiF) yr -= kTwoPiF;
-  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yr, g);
+  torque = lee_attitude_loop(R, Rd, w, e, yr, g);
 }
 
 // LeeVelocityController.__call__ (controllers/velocity_control.py:17-112).
 OUZ_HD void lee_velocity(Q4 q, V3 v, V3 w, V3 cmd_v, float yaw_rate, const LeeGains& g, float& thrust,
                          V3& torque) {
   M3 R = quat_to_mat(q);
-  float roll, pitch, yaw;
-  mat_to_rpy(R, roll, pitch, yaw);
-  M3 Rv = rpy_to_mat(yaw, 0.0f, 0.0f);
-  V3 vv = mtv(Rv, v);
+  EulerSC e = euler_sc(R);
+  // vehicle frame Rz(yaw): v_vehicle = Rz^T v
+  V3 vv = v3(e.cy * v.x + e.sy * v.y, -e.sy * v.x + e.cy * v.y, v.z);
   V3 a = mul(g.kV, cmd_v - vv);
   a.z += 1.0f;
   thrust = a.x * R.m[2] + a.y * R.m[5] + a.z * R.m[8];
-  float pitch_sp = atan2f(a.x, a.z);
-  float roll_sp = atan2f(-a.y, sqrtf(a.z * a.z + a.x * a.x));
-  M3 Rd = rpy_to_mat(yaw, pitch_sp, roll_sp);
-  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yaw_rate, g);
+  // pitch_sp = atan2(a0, a2), roll_sp = atan2(-a1, hypot(a0, a2)) (:58-60) as sin/cos
+  float spt, cpt, srl, crl;
+  unit2(a.x, a.z, spt, cpt);
+  unit2(-a.y, sqrtf(a.z * a.z + a.x * a.x), srl, crl);
+  M3 Rd = rpy_to_mat_sc(e.cy, e.sy, cpt, spt, crl, srl);
+  torque = lee_attitude_loop(R, Rd, w, e, yaw_rate, g);
 }
 
 // LeeAttitudeContoller.__call__ (controllers/attitude_control.py:17-78): cmd = (T, roll, pitch, yaw_rate).
 OUZ_HD void lee_attitude(Q4 q, V3 w, float cmd_t, float cmd_roll, float cmd_pitch, float yaw_rate,
                          const LeeGains& g, float& thrust, V3& torque) {
   M3 R = quat_to_mat(q);
-  float roll, pitch, yaw;
-  mat_to_rpy(R, roll, pitch, yaw);
-  M3 Rd = rpy_to_mat(yaw, cmd_pitch, cmd_roll);
-  torque = lee_attitude_loop(R, Rd, w, roll, pitch, yaw_rate, g);
+  EulerSC e = euler_sc(R);
+  M3 Rd = rpy_to_mat_sc(e.cy, e.sy, cosf(cmd_pitch), sinf(cmd_pitch), cosf(cmd_roll), sinf(cmd_roll));
+  torque = lee_attitude_loop(R, Rd, w, e, yaw_rate, g);
   thrust = cmd_t + 1.0f;
 }
 
@@ -466,27 +488,36 @@ OUZ_HD float reward(V3 p, V3 target, Q4 q, V3 w, float& dist) {
 // ---------------------------------------------------------------------------
 constexpr float kGravity = 9.81f;
 
-OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float mass, V3 I, float dt, int substeps,
-                      float wmax) {
+// f_b / tau_b: body-frame force and torque at the COM (LOCAL_SPACE, ekf_lee_landed.py:525);
+// inv_I = 1/I (diagonal).  Semi-implicit Euler; exact exponential map for the attitude.
+OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m, V3 I, V3 inv_I, float dt,
+                      int substeps, float wmax) {
   const float h = dt / (float)substeps;
-  const float inv_m = 1.0f / mass;
   for (int s = 0; s < substeps; ++s) {
     M3 R = quat_to_mat(q);
     V3 fw = mv(R, f_b);
     v = v + h * v3(fw.x * inv_m, fw.y * inv_m, fw.z * inv_m - kGravity);
     V3 wb = mtv(R, w);
-    V3 Iw = mul(I, wb);
-    V3 c = cross(wb, Iw);
-    V3 wdot = v3((tau_b.x - c.x) / I.x, (tau_b.y - c.y) / I.y, (tau_b.z - c.z) / I.z);
-    wb = wb + h * wdot;
+    V3 c = cross(wb, mul(I, wb));
+    wb = wb + h * mul(inv_I, tau_b - c);
     w = mv(R, wb);
-    float n = norm(w);
-    if (n > wmax) w = (wmax / n) * w;
+    float n2 = dot(w, w);
+    if (n2 > wmax * wmax) w = (wmax / sqrtf(n2)) * w;
     p = p + h * v;
-    n = norm(w);
-    float th = 0.5f * h * n;
-    float sc = (th < 1e-4f) ? 0.5f * h * (1.0f - th * th * (1.0f / 6.0f)) : sinf(th) / n;
-    Q4 dq{w.x * sc, w.y * sc, w.z * sc, cosf(th)};
+    // dq = [sin(th) w/|w|, cos(th)], th = |w| h / 2.  |w| <= wmax keeps th small at the
+    // configured dt (4 pi * 0.005 / 2 = 0.031 rad): there the Taylor series to th^5 / th^6
+    // is exact in f32 and replaces the libm sin/cos.
+    float n = sqrtf(dot(w, w));
+    float th = 0.5f * h * n, th2 = th * th;
+    float sc, co;
+    if (th < 0.1f) {
+      sc = 0.5f * h * (1.0f - th2 * (1.0f / 6.0f) * (1.0f - th2 * (1.0f / 20.0f)));        // sin(th)/|w|
+      co = 1.0f - 0.5f * th2 * (1.0f - th2 * (1.0f / 12.0f) * (1.0f - th2 * (1.0f / 30.0f)));
+    } else {
+      sc = sinf(th) / n;
+      co = cosf(th);
+    }
+    Q4 dq{w.x * sc, w.y * sc, w.z * sc, co};
     q = quat_mul(dq, q);
     float qi = 1.0f / sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
     q = Q4{q.x * qi, q.y * qi, q.z * qi, q.w * qi};

@@ -166,9 +166,32 @@ class QuadVecTask:
         """(N, 13) view [p, q_xyzw, v, w] of the SoA state (ekf_lee_landed.py:84)."""
         return self.fstate[0:13].t()
 
+    def env_task_ids(self):
+        """Per-env task id (the mixed curriculum assigns tasks per 64-env block of global ids)."""
+        gid = torch.arange(self.num_envs, device=self.device) + int(self.cfg.env_id_offset)
+        if self.task != L.TASK_MIXED:
+            return torch.full_like(gid, self.task)
+        tasks = torch.tensor(L.MIXED_TASKS, device=self.device)
+        return tasks[(gid // L.MIXED_CHUNK) % len(L.MIXED_TASKS)]
+
     @property
     def target_root_positions(self):
-        return self.fstate[L.F_TARGET:L.F_TARGET + 3].t()
+        """(N, 3) target_root_positions.  Random goals are stored state; a landing-platform target
+        is platform xy + offset at z 0.377 and is recomputed here (the kernel never stores it)."""
+        tgt = self.fstate[L.F_TARGET:L.F_TARGET + 3].t().clone()
+        tids = self.env_task_ids()
+        started = self.sim_step_count > 0
+        for t in tids.unique().tolist():
+            info = task_info(t)
+            if info.target_mode == L.TGT_GOAL:
+                continue
+            m = tids == t
+            plat = self.fstate[L.F_PLAT:L.F_PLAT + 2].t()[m] if info.target_mode == L.TGT_TRAJ else \
+                torch.zeros((int(m.sum()), 2), device=self.device)
+            tgt[m, 0] = plat[:, 0] + info.plat_offset_x if started else 0.0
+            tgt[m, 1] = plat[:, 1] if started else 0.0
+            tgt[m, 2] = 0.377
+        return tgt
 
     @property
     def sim_step_count(self) -> int:

@@ -153,7 +153,48 @@ def gen_ekf(ref):
     np.savez_compressed(os.path.join(HERE, "ekf.npz"), **out)
 
 
+def _run_pv(mod, dtype, g_in, dt):
+    """Drive the reference PVFilter exactly like ekf_lee_landed.py:417-444 (shared trigger counters)."""
+    x0, acc, qn, pos, vel, flip = g_in
+    n_env, T = x0.shape[0], acc.shape[0]
+    acc_var = torch.tensor([0.01, 0.01, 0.01], dtype=dtype) * 100
+    fl = [mod.PVFilter(acc_var, "cpu") for _ in range(n_env)]
+    for e in range(n_env):
+        fl[e].set_states(torch.tensor(x0[e], dtype=dtype).reshape(9, 1))
+    xs = np.zeros((T, n_env, 9))
+    Ps = np.zeros((T, n_env, 9, 9))
+    trig_p = np.zeros((T, n_env), bool)
+    trig_v = np.zeros((T, n_env), bool)
+    pos_var = torch.tensor([1.0, 1.0, 1.0], dtype=dtype) * 0.0000001
+    cp, cv = 0, 75 / 2                                        # ekf_lee_landed.py:153-154
+    for t in range(T):
+        for e in range(n_env):
+            q_in = qn[t, e]
+            if flip[t]:
+                q_in = q_in[[1, 2, 3, 0]]                     # give xyzw; the filter flips to wxyz
+            fl[e].prediction_step(torch.tensor(acc[t, e], dtype=dtype), torch.tensor(q_in, dtype=dtype), dt=dt,
+                                  flip_Qw=bool(flip[t]))
+            tp = True & ((cp * dt) > (1 / 20))
+            tv = True & ((cv * dt) > (1 / 75))
+            if tp:
+                fl[e].correction_step(gps_data=torch.tensor(pos[t, e], dtype=dtype), gps_var=pos_var)
+                cp = 0
+            else:
+                cp += 1
+            if tv:
+                fl[e].correction_step(vel_data=torch.tensor(vel[t, e], dtype=dtype), vel_var=pos_var)
+                cv = 0
+            else:
+                cv += 1
+            trig_p[t, e], trig_v[t, e] = tp, tv
+            xs[t, e] = fl[e].get_states().numpy().reshape(9)
+            Ps[t, e] = fl[e].get_covariances().numpy()
+    return xs, Ps, trig_p, trig_v
+
+
 def gen_pv(ref):
+    """Float64 run = the algorithm; the reference's own float32 run is stored too (x_f32ref,
+    P_f32ref) to show how far an f32 evaluation of its literal (I - K H) P drifts."""
     torch.set_default_dtype(torch.float64)
     try:
         mod = _load("ref_pvfilter", os.path.join(ref, "isaacgymenvs", "PVFilter.py"))
@@ -162,11 +203,7 @@ def gen_pv(ref):
         for seed in (0, 1, 2):
             rs = np.random.RandomState(3000 + seed)
             n_env, T = 13, 28
-            acc_var = torch.tensor([0.01, 0.01, 0.01]) * 100
-            fl = [mod.PVFilter(acc_var, "cpu") for _ in range(n_env)]
             x0 = np.concatenate([rs.normal(0, 1, (n_env, 3)), rs.normal(0, 0.3, (n_env, 3)), np.zeros((n_env, 3))], 1)
-            for e in range(n_env):
-                fl[e].set_states(torch.tensor(x0[e]).reshape(9, 1))
             acc = rs.normal(0, 1, (T, n_env, 3)) + np.array([0, 0, 9.8])
             qn = rs.normal(0, 1, (T, n_env, 4))
             qn[..., 0] += 3.0
@@ -174,36 +211,15 @@ def gen_pv(ref):
             pos = rs.normal(0, 1, (T, n_env, 3))
             vel = rs.normal(0, 0.3, (T, n_env, 3))
             flip = np.array([t < 10 for t in range(T)])               # xyzw input during "convergence"
-            xs = np.zeros((T, n_env, 9))
-            Ps = np.zeros((T, n_env, 9, 9))
-            trig_p = np.zeros((T, n_env), bool)
-            trig_v = np.zeros((T, n_env), bool)
-            pos_var = torch.tensor([1.0, 1.0, 1.0]) * 0.0000001
-            cp, cv = 0, 75 / 2                                        # ekf_lee_landed.py:153-154
-            for t in range(T):
-                for e in range(n_env):
-                    q_in = qn[t, e]
-                    if flip[t]:
-                        q_in = q_in[[1, 2, 3, 0]]                     # give xyzw; filter flips to wxyz
-                    fl[e].prediction_step(torch.tensor(acc[t, e]), torch.tensor(q_in), dt=dt, flip_Qw=bool(flip[t]))
-                    tp = True & ((cp * dt) > (1 / 20))
-                    tv = True & ((cv * dt) > (1 / 75))
-                    if tp:
-                        fl[e].correction_step(gps_data=torch.tensor(pos[t, e]), gps_var=pos_var)
-                        cp = 0
-                    else:
-                        cp += 1
-                    if tv:
-                        fl[e].correction_step(vel_data=torch.tensor(vel[t, e]), vel_var=pos_var)
-                        cv = 0
-                    else:
-                        cv += 1
-                    trig_p[t, e], trig_v[t, e] = tp, tv
-                    xs[t, e] = fl[e].get_states().numpy().reshape(9)
-                    Ps[t, e] = fl[e].get_covariances().numpy()
+            g_in = (x0, acc, qn, pos, vel, flip)
+            xs, Ps, trig_p, trig_v = _run_pv(mod, torch.float64, g_in, dt)
+            torch.set_default_dtype(torch.float32)
+            xs32, Ps32, _, _ = _run_pv(mod, torch.float32, g_in, dt)
+            torch.set_default_dtype(torch.float64)
             out.update({f"s{seed}_x0": x0, f"s{seed}_acc": acc, f"s{seed}_q_wxyz": qn, f"s{seed}_pos": pos,
                         f"s{seed}_vel": vel, f"s{seed}_x": xs, f"s{seed}_P": Ps, f"s{seed}_trig_p": trig_p,
-                        f"s{seed}_trig_v": trig_v})
+                        f"s{seed}_trig_v": trig_v, f"s{seed}_x_f32ref": xs32.astype(np.float32),
+                        f"s{seed}_P_f32ref": Ps32.astype(np.float32)})
         out["dt"] = np.array(dt)
         np.savez_compressed(os.path.join(HERE, "pvfilter.npz"), **out)
     finally:

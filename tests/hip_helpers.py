@@ -49,7 +49,7 @@ def gpu_to_oracle(env, oenv):
     oenv.q = f[L.F_Q:L.F_Q + 4].T.copy()
     oenv.v = f[L.F_V:L.F_V + 3].T.copy()
     oenv.w = f[L.F_W:L.F_W + 3].T.copy()
-    oenv.target = f[L.F_TARGET:L.F_TARGET + 3].T.copy()
+    oenv.target = env.target_root_positions.cpu().numpy().astype(np.float64)
     oenv.prev_v = f[L.F_PREV_V:L.F_PREV_V + 3].T.copy()
     oenv.thrust = f[L.F_THRUST:L.F_THRUST + 4].T.copy()
     oenv.ekf_q = f[L.F_EKF_Q:L.F_EKF_Q + 4].T.copy()
@@ -79,7 +79,7 @@ def gpu_snapshot(env):
     iv = env.istate.cpu().numpy()
     return {
         "p": f[0:3].T, "q": f[3:7].T, "v": f[7:10].T, "w": f[10:13].T,
-        "target": f[L.F_TARGET:L.F_TARGET + 3].T, "thrust": f[L.F_THRUST:L.F_THRUST + 4].T,
+        "target": env.target_root_positions.cpu().numpy().astype(np.float64), "thrust": f[L.F_THRUST:L.F_THRUST + 4].T,
         "ekf_q": f[L.F_EKF_Q:L.F_EKF_Q + 4].T, "pv_x": f[L.F_PV_X:L.F_PV_X + 9].T,
         "waypoint": f[L.F_WAYPOINT:L.F_WAYPOINT + 3].T, "plat": f[L.F_PLAT:L.F_PLAT + 2].T,
         "progress": iv[L.I_PROGRESS], "land_flag": iv[L.I_LAND_FLAG],

@@ -96,6 +96,7 @@ def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
     x = t(g[f"s{seed}_x0"])
     n = x.shape[0]
     P = t(pack_sym(np.broadcast_to(np.eye(9) * Q.PV_P0, (n, 9, 9)), 9))
+    err_ours = err_ref32 = 0.0
     for step in range(g[f"s{seed}_acc"].shape[0]):
         acc, qw = t(g[f"s{seed}_acc"][step]), t(g[f"s{seed}_q_wxyz"][step])
         L.check(L.lib.ouz_pv_predict(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, n, stream()))
@@ -108,15 +109,19 @@ def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
         gx, gP = g[f"s{seed}_x"][step], g[f"s{seed}_P"][step]
         hx = x.cpu().numpy().astype(np.float64)
         hP = unpack_sym(P.cpu().numpy().astype(np.float64), 9)
-        # The reference's literal (I-KH)P is ill-conditioned (P0=1e3 vs R=1e-7); even two f64
-        # evaluations agree only to ~3e-7 of the state magnitude.  The f32 stable form is held
-        # to 2e-4 of each env's state magnitude, and its covariance to 1e-3 of the env's largest
-        # entry: the first position fixes cancel P_bb ~ 1e3 down to ~0.4, so f32 keeps ~1e-4
-        # relative there (2400 x eps_f32), which any f32 evaluation -- the reference's own torch
-        # f32 run included -- loses.
+        # The reference's literal (I-KH)P is ill-conditioned (P0=1e3 vs R=1e-7).  Its OWN float32
+        # torch run (golden x_f32ref/P_f32ref) drifts from the float64 run by up to ~2x the state
+        # magnitude and ~20% of the covariance (test_oracle_golden.py pins that).  The f32 stable
+        # form here is held to 1e-3 of each env's state / covariance magnitude: the first position
+        # fixes cancel P_bb ~ 1e3 down to ~0.4, which costs any f32 evaluation ~2400 eps_f32.
         for e in range(n):
-            assert np.abs(hx[e] - gx[e]).max() <= 2e-4 * max(1.0, np.abs(gx[e]).max()), (step, e)
+            assert np.abs(hx[e] - gx[e]).max() <= 1e-3 * max(1.0, np.abs(gx[e]).max()), (step, e)
             assert np.abs(hP[e] - gP[e]).max() <= 1e-3 * np.abs(gP[e]).max(), (step, e)
+        err_ours = max(err_ours, max(np.abs(hx[e] - gx[e]).max() / max(1.0, np.abs(gx[e]).max()) for e in range(n)))
+        gx32 = g[f"s{seed}_x_f32ref"][step].astype(np.float64)
+        err_ref32 = max(err_ref32, max(np.abs(gx32[e] - gx[e]).max() / max(1.0, np.abs(gx[e]).max()) for e in range(n)))
+    # ours is at least 100x closer to the float64 algorithm than the reference's own float32 run
+    assert err_ours * 100 <= err_ref32, (err_ours, err_ref32)
 
 
 def test_integrate_vs_oracle(L):

@@ -76,3 +76,14 @@ def test_trajectories_and_quat_rotate(golden):
     np.testing.assert_allclose(cir, g["circle"], atol=1e-6)
     np.testing.assert_array_equal(sq, g["square"])
     np.testing.assert_allclose(Q.quat_rotate_xyzw(g["quat_xyzw"], g["vec"]), g["quat_rotate"], atol=1e-12)
+
+
+def test_reference_f32_pvfilter_is_ill_conditioned(golden):
+    """Documents why the HIP PV filter uses the stable update form: the reference's own
+    float32 evaluation of (I - K H) P (torch f32, PVFilter.py:67-110) drifts far from its
+    float64 evaluation on the same inputs."""
+    g = golden("pvfilter.npz")
+    for seed in (0, 1, 2):
+        x, x32 = g[f"s{seed}_x"], g[f"s{seed}_x_f32ref"].astype(np.float64)
+        rel = np.abs(x32 - x).max(-1) / np.maximum(1.0, np.abs(x).max(-1))
+        assert rel.max() > 0.1
