@@ -21,6 +21,8 @@
 #include "../../include/ouzelum.h"
 #include "quad_math.h"
 
+#define OUZ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
 namespace ouz {
 
 enum Ctrl { CTRL_RL = 0, CTRL_LEE_TRUE = 1, CTRL_LEE_EST = 2 };
@@ -304,6 +306,12 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
       eq = EkfQ{eq.w * inv, eq.x * inv, eq.y * inv, eq.z * inv};
     }
     ekf_update(eq, eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, eP[k]);
+    st(a, OUZ_F_EKF_Q, i, eq.w); st(a, OUZ_F_EKF_Q + 1, i, eq.x); st(a, OUZ_F_EKF_Q + 2, i, eq.y); st(a, OUZ_F_EKF_Q + 3, i, eq.z);
+    // Phase fence: keeps the scheduler from hoisting the 45 PV-covariance loads above the EKF
+    // (it would otherwise hold ~100 state floats live across every phase: 408 registers, 1 wave/SIMD).
+    OUZ_SCHED_FENCE();
     EkfQ orient = eq;
     float pm[3] = {p.x, p.y, p.z}, vm[3] = {v.x, v.y, v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
     if (conv) {
@@ -325,9 +333,7 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
     for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_X + k, i, px[k]);
 #pragma unroll
     for (int k = 0; k < 45; ++k) st(a, OUZ_F_PV_P + k, i, pP[k]);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, eP[k]);
-    st(a, OUZ_F_EKF_Q, i, eq.w); st(a, OUZ_F_EKF_Q + 1, i, eq.x); st(a, OUZ_F_EKF_Q + 2, i, eq.y); st(a, OUZ_F_EKF_Q + 3, i, eq.z);
+    OUZ_SCHED_FENCE();
     // waypoint guidance (:464-492)
     V3 wp = conv ? target : ld3(a, OUZ_F_WAYPOINT, i);
     V3 tv = target - p;
@@ -491,7 +497,7 @@ __global__ void mark_all_kernel(int64_t* reset, int32_t n) {
 // ---------------------------------------------------------------------------
 // component kernels (AoS in/out; parity entry points)
 // ---------------------------------------------------------------------------
-__global__ void lee_kernel(int mode, const float* s, const float* cmd, float* thrust, float* torque, int n) {
+__global__ void __launch_bounds__(64) lee_kernel(int mode, const float* s, const float* cmd, float* thrust, float* torque, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float* x = s + (size_t)i * 13;
@@ -508,44 +514,54 @@ __global__ void lee_kernel(int mode, const float* s, const float* cmd, float* th
   torque[i * 3 + 0] = tau.x; torque[i * 3 + 1] = tau.y; torque[i * 3 + 2] = tau.z;
 }
 
-__global__ void ekf_kernel(const float* q, const float* P, const float* gyr, const float* ang, float dt, float* qo,
+__global__ void __launch_bounds__(64) ekf_kernel(const float* q, const float* P, const float* gyr, const float* ang, float dt, float* qo,
                            float* Po, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   EkfQ e{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]};
   float p[10];
+  #pragma unroll
   for (int k = 0; k < 10; ++k) p[k] = P[i * 10 + k];
   ekf_update(e, p, v3(gyr[i * 3], gyr[i * 3 + 1], gyr[i * 3 + 2]), EkfQ{ang[i * 4], ang[i * 4 + 1], ang[i * 4 + 2], ang[i * 4 + 3]}, dt);
   qo[i * 4] = e.w; qo[i * 4 + 1] = e.x; qo[i * 4 + 2] = e.y; qo[i * 4 + 3] = e.z;
+  #pragma unroll
   for (int k = 0; k < 10; ++k) Po[i * 10 + k] = p[k];
 }
 
-__global__ void pv_predict_kernel(float* x, float* P, const float* acc, const float* q, float dt, int n) {
+__global__ void __launch_bounds__(64) pv_predict_kernel(float* x, float* P, const float* acc, const float* q, float dt, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float xx[9], pp[45];
+  #pragma unroll
   for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+  #pragma unroll
   for (int k = 0; k < 45; ++k) pp[k] = P[i * 45 + k];
   pv_predict(xx, pp, v3(acc[i * 3], acc[i * 3 + 1], acc[i * 3 + 2]), EkfQ{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]}, dt);
+  #pragma unroll
   for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+  #pragma unroll
   for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
 }
 
-__global__ void pv_correct_kernel(float* x, float* P, const float* z, int block, float var, const uint8_t* mask, int n) {
+__global__ void __launch_bounds__(64) pv_correct_kernel(float* x, float* P, const float* z, int block, float var, const uint8_t* mask, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (mask && !mask[i]) return;
   float xx[9], pp[45];
+  #pragma unroll
   for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+  #pragma unroll
   for (int k = 0; k < 45; ++k) pp[k] = P[i * 45 + k];
   V3 zz = v3(z[i * 3], z[i * 3 + 1], z[i * 3 + 2]);
   if (block == 0) pv_correct<0>(xx, pp, zz, var);
   else pv_correct<1>(xx, pp, zz, var);
+  #pragma unroll
   for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+  #pragma unroll
   for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
 }
 
-__global__ void integrate_kernel(float* root, const float* fb, const float* tb, const float* mass, const float* inertia,
+__global__ void __launch_bounds__(64) integrate_kernel(float* root, const float* fb, const float* tb, const float* mass, const float* inertia,
                                  float dt, int substeps, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -559,7 +575,7 @@ __global__ void integrate_kernel(float* root, const float* fb, const float* tb, 
   s[7] = v.x; s[8] = v.y; s[9] = v.z; s[10] = w.x; s[11] = w.y; s[12] = w.z;
 }
 
-__global__ void reward_kernel(const float* root, const float* target, const int32_t* progress, int max_ep, float z_die,
+__global__ void __launch_bounds__(64) reward_kernel(const float* root, const float* target, const int32_t* progress, int max_ep, float z_die,
                               float* rew, int64_t* reset, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -572,7 +588,7 @@ __global__ void reward_kernel(const float* root, const float* target, const int3
   reset[i] = (progress[i] >= max_ep - 1 || die) ? 1 : 0;
 }
 
-__global__ void philox_kernel(uint64_t seed, const uint32_t* env, uint32_t step, uint32_t stream, uint32_t sub, uint32_t* out, int n) {
+__global__ void __launch_bounds__(64) philox_kernel(uint64_t seed, const uint32_t* env, uint32_t step, uint32_t stream, uint32_t sub, uint32_t* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   U4 r = draw(seed, env[i], step, stream, sub);

@@ -402,33 +402,55 @@ constexpr float kPvAccVar = 1.0f;     // [0.01]*3 * 100 (ekf_lee_landed.py:137)
 constexpr float kPvPosVar = 1e-7f;    // ekf_lee_landed.py:408
 constexpr float kPvP0 = 1000.0f;      // PVFilter.py:12
 
+// Scheduling fence between phases of one env's math: the AMDGPU scheduler otherwise
+// interleaves independent 3x3 block products and holds all their temporaries live.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define OUZ_PHASE() ((void)0)
+#else
+#define OUZ_PHASE() ((void)0)
+#endif
+
 // prediction_step: M = R(q/|q|)^T; F = [[I, M dt, M h],[0, M, M dt],[0,0,I]], G = F[:, 6:9] (rows 0..5),
 // x = F x + G (a - b); P = F P F^T + q_a G G^T.   (h = dt^2/2)
+// Block form, P = [[A, B, C], [B^T, D, E], [C^T, E^T, Fb]]:
+//   T13 = C + M (dt E + h Fb)   T12 = B + M (dt D + h E^T)   T11 = A + M (dt B^T + h C^T)
+//   T23 = M (E + dt Fb)         T22 = M (D + dt E^T)
+//   A' = T11 + (dt T12 + h T13) M^T + q h^2 M M^T     B' = (T12 + dt T13) M^T + q h dt M M^T
+//   D' = (T22 + dt T23) M^T + q dt^2 M M^T             C' = T13, E' = T23, Fb' = Fb
 OUZ_HD void pv_predict(float x[9], float P[45], V3 acc, EkfQ q, float dt) {
   float inv = 1.0f / sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
-  M3 M = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
+  const M3 M = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
   const float h = dt * dt * 0.5f;
-  V3 xp = v3(x[0], x[1], x[2]), xv = v3(x[3], x[4], x[5]), xb = v3(x[6], x[7], x[8]);
-  V3 u = acc - xb;
-  V3 np_ = xp + mv(M, dt * xv) + mv(M, h * xb) + mv(M, h * u);
-  V3 nv = mv(M, xv) + mv(M, dt * xb) + mv(M, dt * u);
-  x[0] = np_.x; x[1] = np_.y; x[2] = np_.z;
-  x[3] = nv.x; x[4] = nv.y; x[5] = nv.z;
-  // block algebra
-  M3 P11 = pblk(P, 0, 0), P12 = pblk(P, 0, 1), P13 = pblk(P, 0, 2);
-  M3 P22 = pblk(P, 1, 1), P23 = pblk(P, 1, 2), P33 = pblk(P, 2, 2);
-  M3 P21 = tr(P12), P31 = tr(P13), P32 = tr(P23);
-  M3 T13 = madd(P13, mm(M, madd(mscale(dt, P23), mscale(h, P33))));
-  M3 T12 = madd(P12, mm(M, madd(mscale(dt, P22), mscale(h, P32))));
-  M3 T11 = madd(P11, mm(M, madd(mscale(dt, P21), mscale(h, P31))));
-  M3 T23 = mm(M, madd(P23, mscale(dt, P33)));
-  M3 T22 = mm(M, madd(P22, mscale(dt, P32)));
-  M3 MMt = mmt(M, M);
-  M3 N11 = madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(kPvAccVar * h * h, MMt));
-  M3 N12 = madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(kPvAccVar * h * dt, MMt));
-  M3 N22 = madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(kPvAccVar * dt * dt, MMt));
-  pset(P, 0, 0, N11); pset(P, 0, 1, N12); pset(P, 0, 2, T13);
-  pset(P, 1, 1, N22); pset(P, 1, 2, T23);
+  {
+    V3 xp = v3(x[0], x[1], x[2]), xv = v3(x[3], x[4], x[5]), xb = v3(x[6], x[7], x[8]);
+    V3 u = acc - xb;
+    V3 np_ = xp + mv(M, dt * xv) + mv(M, h * xb) + mv(M, h * u);
+    V3 nv = mv(M, xv) + mv(M, dt * xb) + mv(M, dt * u);
+    x[0] = np_.x; x[1] = np_.y; x[2] = np_.z;
+    x[3] = nv.x; x[4] = nv.y; x[5] = nv.z;
+  }
+  const M3 MMt = mmt(M, M);
+  OUZ_PHASE();
+  M3 T13 = madd(pblk(P, 0, 2), mm(M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2)))));
+  OUZ_PHASE();
+  M3 T12 = madd(pblk(P, 0, 1), mm(M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1)))));
+  OUZ_PHASE();
+  {
+    M3 T11 = madd(pblk(P, 0, 0), mm(M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0)))));
+    OUZ_PHASE();
+    pset(P, 0, 0, madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(kPvAccVar * h * h, MMt)));
+  }
+  OUZ_PHASE();
+  pset(P, 0, 1, madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(kPvAccVar * h * dt, MMt)));
+  OUZ_PHASE();
+  M3 T23 = mm(M, madd(pblk(P, 1, 2), mscale(dt, pblk(P, 2, 2))));
+  OUZ_PHASE();
+  M3 T22 = mm(M, madd(pblk(P, 1, 1), mscale(dt, pblk(P, 2, 1))));
+  OUZ_PHASE();
+  pset(P, 1, 1, madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(kPvAccVar * dt * dt, MMt)));
+  pset(P, 0, 2, T13);
+  pset(P, 1, 2, T23);
+  OUZ_PHASE();
 }
 
 // correction_step for one measured block m (0 = position, 1 = velocity) with R = r I.
@@ -440,31 +462,36 @@ template <int MB>
 OUZ_HD void pv_correct(float x[9], float P[45], V3 z, float r) {
   constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
   constexpr int B = 2;
-  M3 Pmm = pblk(P, MB, MB);
-  M3 S = Pmm;
-  S.m[0] += r; S.m[4] += r; S.m[8] += r;
-  M3 Si = inv_sym3(S);
-  M3 PmA = pblk(P, MB, A), PmB = pblk(P, MB, B);     // P_{m,o}
-  M3 KA = mm(tr(PmA), Si), KB = mm(tr(PmB), Si);     // K_o = P_{o,m} S^-1
-  V3 xm = v3(x[MB * 3 + 0], x[MB * 3 + 1], x[MB * 3 + 2]);
-  V3 y = z - xm;
-  V3 nm = z - r * mv(Si, y);
-  V3 dA = mv(KA, y), dB = mv(KB, y);
-  x[MB * 3 + 0] = nm.x; x[MB * 3 + 1] = nm.y; x[MB * 3 + 2] = nm.z;
-  x[A * 3 + 0] += dA.x; x[A * 3 + 1] += dA.y; x[A * 3 + 2] += dA.z;
-  x[B * 3 + 0] += dB.x; x[B * 3 + 1] += dB.y; x[B * 3 + 2] += dB.z;
-  M3 PAA = pblk(P, A, A), PAB = pblk(P, A, B), PBB = pblk(P, B, B);
-  M3 nAA = msub(PAA, mm(KA, PmA));
-  M3 nAB = msub(PAB, mm(KA, PmB));
-  M3 nBB = msub(PBB, mm(KB, PmB));
+  M3 Si;
+  {
+    M3 S = pblk(P, MB, MB);
+    S.m[0] += r; S.m[4] += r; S.m[8] += r;
+    Si = inv_sym3(S);
+  }
+  OUZ_PHASE();
+  const M3 KA = mm(pblk(P, A, MB), Si), KB = mm(pblk(P, B, MB), Si);     // K_o = P_{o,m} S^-1
+  {
+    V3 y = z - v3(x[MB * 3 + 0], x[MB * 3 + 1], x[MB * 3 + 2]);
+    V3 nm = z - r * mv(Si, y);
+    V3 dA = mv(KA, y), dB = mv(KB, y);
+    x[MB * 3 + 0] = nm.x; x[MB * 3 + 1] = nm.y; x[MB * 3 + 2] = nm.z;
+    x[A * 3 + 0] += dA.x; x[A * 3 + 1] += dA.y; x[A * 3 + 2] += dA.z;
+    x[B * 3 + 0] += dB.x; x[B * 3 + 1] += dB.y; x[B * 3 + 2] += dB.z;
+  }
+  OUZ_PHASE();
+  // other-other blocks first: they read P_{m,o}, which is overwritten below
+  pset(P, B, B, msub(pblk(P, B, B), mm(KB, pblk(P, MB, B))));
+  OUZ_PHASE();
+  pset(P, A, B, msub(pblk(P, A, B), mm(KA, pblk(P, MB, B))));
+  OUZ_PHASE();
+  pset(P, A, A, msub(pblk(P, A, A), mm(KA, pblk(P, MB, A))));
+  OUZ_PHASE();
+  // P_{m,o} = r S^-1 P_{m,o} = r K_o^T
+  if (MB < A) pset(P, MB, A, mscale(r, tr(KA))); else pset(P, A, MB, mscale(r, KA));
+  pset(P, MB, B, mscale(r, tr(KB)));
   M3 I3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
-  M3 nmm = mscale(r, msub(I3, mscale(r, Si)));
-  M3 nmA = mscale(r, mm(Si, PmA));
-  M3 nmB = mscale(r, mm(Si, PmB));
-  pset(P, MB, MB, nmm);
-  if (MB < A) pset(P, MB, A, nmA); else pset(P, A, MB, tr(nmA));
-  pset(P, MB, B, nmB);
-  pset(P, A, A, nAA); pset(P, A, B, nAB); pset(P, B, B, nBB);
+  pset(P, MB, MB, mscale(r, msub(I3, mscale(r, Si))));
+  OUZ_PHASE();
 }
 
 // ---------------------------------------------------------------------------

@@ -1,0 +1,90 @@
+"""world_size-2 gloo tests of the N>1 path on CPU.
+
+The step itself never communicates; what must hold across ranks is (1) the env
+sharding — rank r simulating global ids [r*N, (r+1)*N) reproduces the unsharded
+run exactly, because every draw and the PV trigger index use the global id — and
+(2) the one collective, the all-reduce of [sum of finished-episode returns, count].
+Sharding is exercised with the CPU oracle (the HIP env needs a GPU; its own
+shard-invariance test is tests/test_gpu_env.py::test_shard_invariance).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import quad_oracle as Q
+
+N_LOCAL = 96
+STEPS = 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, task, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from ouzelum_amd.distributed import allreduce_returns, init_from_env, shard
+    r, w, _ = init_from_env(backend="gloo")
+    assert (r, w) == (rank, world)
+    off, total = shard(N_LOCAL, rank, world)
+    env = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=N_LOCAL, seed=5, env_id_offset=off,
+                                  num_envs_total=total, convergence_time=8))
+    rs = np.random.RandomState(1)
+    ep_sum = np.zeros(N_LOCAL)
+    ep_ret = np.zeros(N_LOCAL)
+    ep_cnt = 0
+    for _ in range(STEPS):
+        a = rs.uniform(-1, 1, (total, 4))[off:off + N_LOCAL]
+        _, rew, reset, _ = env.step(a)
+        ep_ret += rew
+        done = reset != 0
+        ep_sum[done] += ep_ret[done]
+        ep_cnt += int(done.sum())
+        ep_ret[done] = 0
+    stats = torch.tensor([ep_sum.sum(), float(ep_cnt)], dtype=torch.float64)
+    mean = allreduce_returns(stats)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), p=env.p, q=env.q, obs=env.obs, reset=env.reset_buf,
+             stats=stats.numpy(), mean=mean)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("task", ["EKFLeeLanded", "QuadMixed"])
+def test_two_rank_sharding_matches_single_process(tmp_path, task):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), task, str(tmp_path)), nprocs=world, join=True)
+    full = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=N_LOCAL * world, seed=5, convergence_time=8))
+    rs = np.random.RandomState(1)
+    tot_sum, tot_cnt, ep_ret = 0.0, 0, np.zeros(N_LOCAL * world)
+    for _ in range(STEPS):
+        _, rew, reset, _ = full.step(rs.uniform(-1, 1, (N_LOCAL * world, 4)))
+        ep_ret += rew
+        done = reset != 0
+        tot_sum += ep_ret[done].sum()
+        tot_cnt += int(done.sum())
+        ep_ret[done] = 0
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    np.testing.assert_array_equal(np.concatenate([p["p"] for p in parts]), full.p)
+    np.testing.assert_array_equal(np.concatenate([p["obs"] for p in parts]), full.obs)
+    np.testing.assert_array_equal(np.concatenate([p["reset"] for p in parts]), full.reset_buf)
+    # the all-reduced [sum, count] is the global one on every rank
+    for p in parts:
+        np.testing.assert_allclose(p["stats"], [tot_sum, tot_cnt], rtol=1e-12)
+        if tot_cnt:
+            assert abs(float(p["mean"]) - tot_sum / tot_cnt) < 1e-9
+
+
+def test_shard_ranges():
+    from ouzelum_amd.distributed import shard
+    assert shard(4096, 0, 8) == (0, 32768)
+    assert shard(4096, 7, 8) == (7 * 4096, 32768)
