@@ -81,7 +81,7 @@ def action_ring(n, dev, seed):
     return (torch.rand((RING, n, 4), device=dev, generator=g) * 2 - 1).contiguous()
 
 
-def kernel_time_us(env, ring, reps=200):
+def kernel_time_us(env, ring, reps=200, fused=False):
     """Average duration of one step kernel from HIP events on the stream the kernel runs on.
 
     The stream is first held by a spin kernel so that all ``reps`` launches (one
@@ -96,7 +96,7 @@ def kernel_time_us(env, ring, reps=200):
     except Exception:  # noqa: BLE001
         pass
     s.record()
-    env.rollout(ring, reps)
+    env.rollout(ring, reps, fused=fused)
     e.record()
     torch.cuda.synchronize(dev)
     return s.elapsed_time(e) * 1e3 / reps
@@ -158,33 +158,44 @@ def main():
     env = make_env(args.task, n, dev, args.seed, off, total)
     ring = action_ring(n, dev, args.seed + rank)
 
-    def rollouts(steps):
+    storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
+               torch.empty((RING, n), dtype=torch.int64, device=dev), torch.empty((RING, n), dtype=torch.bool, device=dev))
+
+    def rollouts(steps, fused=False):
         done = 0
-        mean_ret = float("nan")
         while done < steps:
             k = min(RING, steps - done)
-            env.rollout(ring, k)
+            if fused:   # learner-style rollout: 16 steps into (16, N, ...) storage, state kept in registers
+                env.rollout(ring, k, fused=True, storage=tuple(t[:k] for t in storage))
+            else:       # one kernel launch per VecTask.step
+                env.rollout(ring, k)
             stats = env.episode_stats()
             if world > 1:
                 dist.all_reduce(stats)
             done += k
-        return mean_ret
+
+    def timed(steps, fused=False):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        rollouts(steps, fused)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     rollouts(args.warmup)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    rollouts(args.steps)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = timed(args.steps)
     value = n * world * args.steps / el
+    rollouts(args.warmup, fused=True)
+    el_fused = timed(args.steps, fused=True)
+    value_fused = n * world * args.steps / el_fused
 
     # secondary: the same steps through the Python VecTask.step() API (one ctypes call each)
     py_rate = None
@@ -214,6 +225,11 @@ def main():
                    "parallelism": f"env-sharded dp{world} (RCCL return all-reduce per 16-step rollout)"},
         "roofline": roofline_entry(args.task, n, us),
         "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
+        "fused_rollout": {"value": round(value_fused, 1), "unit": "env-steps/s",
+                          "ms_per_step": round(el_fused / args.steps * 1e3, 5),
+                          "kernel_us_per_step": round(kernel_time_us(env, ring, 320, fused=True), 3),
+                          "note": "ouz_rollout: 16 steps per launch into (16, N, ...) rollout storage, env state in "
+                                  "registers; same steps, same per-step outputs"},
     }
     if world == 1 and not args.no_sweep:
         sweep = []

@@ -18,8 +18,13 @@
  *   ouz_step        VecTask.step               tasks/base/vec_task.py:313-359
  *                   = pre_physics_step + gym.simulate x controlFrequencyInv + post_physics_step
  *                                              tasks/ekf_lee_landed.py:308-530,620-685
- *   ouz_step_n      K consecutive VecTask.step calls over a ring of action batches
+ *   ouz_step_n      K consecutive VecTask.step calls over a ring of action batches, one launch each
  *                   (the train_vec.py:14-18 env-only loop)
+ *   ouz_rollout     the same K steps fused into launches of up to 32 steps each: env state stays in
+ *                   registers, per-step obs/rew/reset/time_outs go to rollout storage [K][N][...]
+ *                   (the learners' obs[step] = next_obs buffers, PPO/main.py:67-73,88-96) or to the
+ *                   env buffers.  For the Lee tasks actions are ignored (ekf_lee_landed.py:308), so a
+ *                   fused rollout is exactly K VecTask.step calls.
  *   ouz_reset_idx   VecTask.reset_idx / reset_done (lazy: marks reset_buf)
  *                                              tasks/base/vec_task.py:369-406, ekf_lee_landed.py:271-306
  *   ouz_lee_control Controller.__call__        controllers/controller.py:45-48 (+ position/velocity/attitude)
@@ -161,6 +166,8 @@ int ouz_bind(ouz_env* env, const ouz_buffers* bufs);
 int ouz_init_state(ouz_env* env, void* stream);
 int ouz_step(ouz_env* env, const float* actions, void* stream);
 int ouz_step_n(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, void* stream);
+int ouz_rollout(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, float* obs_out,
+                float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, void* stream);
 int ouz_reset_idx(ouz_env* env, const int32_t* env_ids, int32_t n, void* stream);
 int ouz_reset_all(ouz_env* env, void* stream);
 int64_t ouz_get_step(const ouz_env* env);

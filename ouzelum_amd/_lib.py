@@ -79,6 +79,7 @@ SIGNATURES = {
     "ouz_init_state": (_I, [_P, _P]),
     "ouz_step": (_I, [_P, _P, _P]),
     "ouz_step_n": (_I, [_P, _P, _I, _I, _P]),
+    "ouz_rollout": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
     "ouz_reset_all": (_I, [_P, _P]),
     "ouz_get_step": (_I64, [_P]),

@@ -71,18 +71,15 @@ struct EnvConsts {
 struct StepArgs {
   float* f;
   int32_t* iv;
-  const float* actions;
   float* obs;
   float* rew;
   int64_t* reset;
   uint8_t* timeouts;
   const float2* wp_tab;        // lemniscate[100] | circle[100] | square[4]
   int32_t n;
-  uint32_t step;
   uint32_t env_offset;
   uint64_t n_total;
   uint64_t seed;
-  uint32_t flick_mask;         // bit (task*8 + site): batch flicker coin fired this step
   int32_t track_episodes;
   EnvConsts c;
   TaskParams tp[OUZ_NUM_TASKS];
@@ -101,21 +98,29 @@ __device__ __forceinline__ int mixed_task(uint32_t gid) {
   return tasks[(gid / kMixedChunk) % 3];
 }
 
+// Per-step context: the step counter (keys every draw, drives the convergence window),
+// the host-drawn whole-batch flicker coins and this step's action batch.
+struct StepCtx {
+  uint32_t step;
+  uint32_t flick_mask;
+  const float* actions;
+};
+
 // ---------------------------------------------------------------------------
 // POMDP corruption (utils/POMDP.py:23-43) with counter-RNG draws
 // ---------------------------------------------------------------------------
 template <int D>
 __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int task, const StepArgs& a,
-                                            uint32_t gid, uint32_t site, bool per_env_coin) {
+                                            const StepCtx& sc, uint32_t gid, uint32_t site, bool per_env_coin) {
   const int mode = tp.pomdp;
   if (mode == OUZ_POMDP_NONE) return;
   if (mode == OUZ_POMDP_FLICKER || mode == OUZ_POMDP_FLICKER_NOISE) {
     bool fire;
     if (per_env_coin) {
       const float p = (mode == OUZ_POMDP_FLICKER) ? tp.pomdp_prob : 0.1f;
-      fire = unit_f32(draw(a.seed, gid, a.step, RNG_POMDP + site, 0).x) <= p;
+      fire = unit_f32(draw(a.seed, gid, sc.step, RNG_POMDP + site, 0).x) <= p;
     } else {
-      fire = (a.flick_mask >> (task * 8 + site)) & 1u;
+      fire = (sc.flick_mask >> (task * 8 + site)) & 1u;
     }
     if (fire) {
 #pragma unroll
@@ -125,7 +130,7 @@ __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int 
   if (mode == OUZ_POMDP_NOISE || mode == OUZ_POMDP_FLICKER_NOISE) {
 #pragma unroll
     for (int g = 0; g < (D + 3) / 4; ++g) {
-      U4 r = draw(a.seed, gid, a.step, RNG_POMDP + site, 128 + g);
+      U4 r = draw(a.seed, gid, sc.step, RNG_POMDP + site, 128 + g);
       uint32_t w4[4] = {r.x, r.y, r.z, r.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k)
@@ -150,53 +155,161 @@ __device__ __forceinline__ float2 traj_point(const StepArgs& a, int type, int id
 }
 
 // ---------------------------------------------------------------------------
-// The fused step for one env (mirrors oracle/quad_oracle.py::OracleEnv.step)
+// Register-resident state of one env for one task path.  load() reads what the path
+// needs every step; fields that change only on reset / landing / episode end are
+// tracked with dirty bits and written back only when they changed.
+// ---------------------------------------------------------------------------
+enum Dirty : uint32_t { D_DR = 1, D_FAULT = 2, D_TRAJ = 4, D_LAND = 8 };
+
+template <int CTRL, int TGT>
+struct EnvRegs {
+  V3 p, v, w;
+  Q4 q;
+  int32_t progress;
+  bool rst;                       // reset_buf != 0: lazy reset at the start of the next step
+  V3 target;                      // TGT_GOAL: stored random goal
+  float thrust[4];                // CTRL_RL
+  int32_t frot, fonset;           // fault
+  float eta;
+  float dr_m, dr_i, dr_t;         // domain randomisation scales
+  V3 prev_v, wp;                  // CTRL_LEE_EST
+  EkfQ eq;
+  float eP[10], px[9], pP[45];
+  float2 plat;                    // TGT_TRAJ
+  int32_t ttype, tidx;
+  float sd;
+  int32_t land_flag;              // -1: not loaded (only needed on reset / landing)
+  int32_t landings_add, ep_cnt_add;
+  float ep_ret, ep_sum_add;
+  uint32_t dirty;
+};
+
+template <int CTRL, int TGT>
+__device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S) {
+  S.rst = a.reset[i] != 0;
+  S.p = ld3(a, OUZ_F_P, i);
+  S.q = Q4{ld(a, OUZ_F_Q, i), ld(a, OUZ_F_Q + 1, i), ld(a, OUZ_F_Q + 2, i), ld(a, OUZ_F_Q + 3, i)};
+  S.v = ld3(a, OUZ_F_V, i);
+  S.w = ld3(a, OUZ_F_W, i);
+  S.progress = ldi(a, OUZ_I_PROGRESS, i);
+  S.dirty = 0;
+  S.land_flag = -1;
+  S.landings_add = 0;
+  S.ep_cnt_add = 0;
+  S.ep_sum_add = 0.0f;
+  S.ep_ret = a.track_episodes ? ld(a, OUZ_F_EP_RET, i) : 0.0f;
+  S.dr_m = S.dr_i = S.dr_t = 1.0f;
+  if (tp.dr) { S.dr_m = ld(a, OUZ_F_DR, i); S.dr_i = ld(a, OUZ_F_DR + 1, i); S.dr_t = ld(a, OUZ_F_DR + 2, i); }
+  if constexpr (TGT == TGT_GOAL) S.target = ld3(a, OUZ_F_TARGET, i);
+  if constexpr (CTRL == CTRL_RL) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) S.thrust[k] = ld(a, OUZ_F_THRUST + k, i);
+    S.frot = -1; S.fonset = 0; S.eta = 1.0f;
+    if (tp.fault) { S.frot = ldi(a, OUZ_I_FAULT_ROTOR, i); S.fonset = ldi(a, OUZ_I_FAULT_ONSET, i); S.eta = ld(a, OUZ_F_FAULT_ETA, i); }
+  }
+  if constexpr (CTRL == CTRL_LEE_EST) {
+    S.prev_v = ld3(a, OUZ_F_PREV_V, i);
+    S.wp = ld3(a, OUZ_F_WAYPOINT, i);
+    S.eq = EkfQ{ld(a, OUZ_F_EKF_Q, i), ld(a, OUZ_F_EKF_Q + 1, i), ld(a, OUZ_F_EKF_Q + 2, i), ld(a, OUZ_F_EKF_Q + 3, i)};
+#pragma unroll
+    for (int k = 0; k < 10; ++k) S.eP[k] = ld(a, OUZ_F_EKF_P + k, i);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) S.px[k] = ld(a, OUZ_F_PV_X + k, i);
+#pragma unroll
+    for (int k = 0; k < 45; ++k) S.pP[k] = ld(a, OUZ_F_PV_P + k, i);
+  }
+  if constexpr (TGT == TGT_TRAJ) {
+    S.plat = make_float2(ld(a, OUZ_F_PLAT, i), ld(a, OUZ_F_PLAT + 1, i));
+    S.ttype = ldi(a, OUZ_I_TRAJ_TYPE, i);
+    S.tidx = ldi(a, OUZ_I_TRAJ_IDX, i);
+    S.sd = ld(a, OUZ_F_TRAJ_SD, i);
+  } else {
+    S.plat = make_float2(0.0f, 0.0f);
+  }
+}
+
+template <int CTRL, int TGT>
+__device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskParams& tp, const EnvRegs<CTRL, TGT>& S) {
+  st3(a, OUZ_F_P, i, S.p);
+  st(a, OUZ_F_Q, i, S.q.x); st(a, OUZ_F_Q + 1, i, S.q.y); st(a, OUZ_F_Q + 2, i, S.q.z); st(a, OUZ_F_Q + 3, i, S.q.w);
+  st3(a, OUZ_F_V, i, S.v);
+  st3(a, OUZ_F_W, i, S.w);
+  sti(a, OUZ_I_PROGRESS, i, S.progress);
+  if (a.track_episodes) {
+    st(a, OUZ_F_EP_RET, i, S.ep_ret);
+    if (S.ep_cnt_add) {
+      st(a, OUZ_F_EP_SUM, i, ld(a, OUZ_F_EP_SUM, i) + S.ep_sum_add);
+      sti(a, OUZ_I_EP_CNT, i, ldi(a, OUZ_I_EP_CNT, i) + S.ep_cnt_add);
+    }
+  }
+  if (S.landings_add) sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + S.landings_add);
+  if (S.dirty & D_LAND) sti(a, OUZ_I_LAND_FLAG, i, S.land_flag);
+  if (S.dirty & D_DR) { st(a, OUZ_F_DR, i, S.dr_m); st(a, OUZ_F_DR + 1, i, S.dr_i); st(a, OUZ_F_DR + 2, i, S.dr_t); }
+  if constexpr (TGT == TGT_GOAL) st3(a, OUZ_F_TARGET, i, S.target);
+  if constexpr (CTRL == CTRL_RL) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st(a, OUZ_F_THRUST + k, i, S.thrust[k]);
+    if (S.dirty & D_FAULT) { sti(a, OUZ_I_FAULT_ROTOR, i, S.frot); sti(a, OUZ_I_FAULT_ONSET, i, S.fonset); st(a, OUZ_F_FAULT_ETA, i, S.eta); }
+  }
+  if constexpr (CTRL == CTRL_LEE_EST) {
+    st3(a, OUZ_F_PREV_V, i, S.prev_v);
+    st3(a, OUZ_F_WAYPOINT, i, S.wp);
+    st(a, OUZ_F_EKF_Q, i, S.eq.w); st(a, OUZ_F_EKF_Q + 1, i, S.eq.x); st(a, OUZ_F_EKF_Q + 2, i, S.eq.y); st(a, OUZ_F_EKF_Q + 3, i, S.eq.z);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, S.eP[k]);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_X + k, i, S.px[k]);
+#pragma unroll
+    for (int k = 0; k < 45; ++k) st(a, OUZ_F_PV_P + k, i, S.pP[k]);
+  }
+  if constexpr (TGT == TGT_TRAJ) {
+    st(a, OUZ_F_PLAT, i, S.plat.x); st(a, OUZ_F_PLAT + 1, i, S.plat.y);
+    sti(a, OUZ_I_TRAJ_IDX, i, S.tidx);
+    if (S.dirty & D_TRAJ) { sti(a, OUZ_I_TRAJ_TYPE, i, S.ttype); st(a, OUZ_F_TRAJ_SD, i, S.sd); }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One VecTask.step of one env on register state (mirrors oracle/quad_oracle.py::OracleEnv.step)
 // ---------------------------------------------------------------------------
 template <int CTRL, int TGT>
-__device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid, int task, float* ob) {
+__device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
+                                         EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout) {
   const TaskParams& tp = a.tp[task];
   const EnvConsts& c = a.c;
-  const bool rst = a.reset[i] != 0;
-  V3 p = ld3(a, OUZ_F_P, i);
-  Q4 q{ld(a, OUZ_F_Q, i), ld(a, OUZ_F_Q + 1, i), ld(a, OUZ_F_Q + 2, i), ld(a, OUZ_F_Q + 3, i)};
-  V3 v = ld3(a, OUZ_F_V, i);
-  V3 w = ld3(a, OUZ_F_W, i);
-  int32_t progress = ldi(a, OUZ_I_PROGRESS, i);
+  const bool rst = S.rst;
   // target_root_positions: random goals are state (ouzelum.py:180-190); a platform target is
-  // platform xy + offset at z 0.377 (ekf_lee_landed.py:87,628-629) and is recomputed, not stored.
+  // platform xy + offset at z 0.377 (ekf_lee_landed.py:87,628-629), recomputed rather than stored.
   // Before the first post_physics_step it is still (0, 0, 0.377).
   V3 target;
-  if constexpr (TGT == TGT_GOAL) target = ld3(a, OUZ_F_TARGET, i);
-  else target = v3(a.step == 0 ? 0.0f : tp.plat_off_x, 0.0f, 0.377f);
-  float2 plat = make_float2(0.0f, 0.0f);
-  float dr_m = 1.0f, dr_i = 1.0f, dr_t = 1.0f;
-  if (tp.dr) { dr_m = ld(a, OUZ_F_DR, i); dr_i = ld(a, OUZ_F_DR + 1, i); dr_t = ld(a, OUZ_F_DR + 2, i); }
+  if constexpr (TGT == TGT_GOAL) target = S.target;
+  else target = sc.step == 0 ? v3(0.0f, 0.0f, 0.377f) : v3(S.plat.x + tp.plat_off_x, S.plat.y, 0.377f);
 
   // ---- lazy reset (ekf_lee_landed.py:271-306,312-335; ouzelum.py:192-233) ----
   if (rst) {
-    U4 r = draw(a.seed, gid, a.step, RNG_RESET_POS);
-    p = v3(uniform_f32(r.x, -1.5f, 1.5f), uniform_f32(r.y, -1.5f, 1.5f), __fadd_rn(1.0f, uniform_f32(r.z, -0.2f, 1.5f)));
-    q = Q4{0.0f, 0.0f, 0.0f, 1.0f};
-    v = v3(0.0f, 0.0f, 0.0f);
-    w = v3(0.0f, 0.0f, 0.0f);
-    progress = 0;
-    const int32_t lf = ldi(a, OUZ_I_LAND_FLAG, i);     // landing counter (ekf_lee_landed.py:323-331)
-    if (lf) {
-      sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + lf);
-      sti(a, OUZ_I_LAND_FLAG, i, 0);
-    }
+    U4 r = draw(a.seed, gid, sc.step, RNG_RESET_POS);
+    S.p = v3(uniform_f32(r.x, -1.5f, 1.5f), uniform_f32(r.y, -1.5f, 1.5f), __fadd_rn(1.0f, uniform_f32(r.z, -0.2f, 1.5f)));
+    S.q = Q4{0.0f, 0.0f, 0.0f, 1.0f};
+    S.v = v3(0.0f, 0.0f, 0.0f);
+    S.w = v3(0.0f, 0.0f, 0.0f);
+    S.progress = 0;
+    if (S.land_flag < 0) S.land_flag = ldi(a, OUZ_I_LAND_FLAG, i);   // landing counter (ekf_lee_landed.py:323-331)
+    if (S.land_flag) { S.landings_add += S.land_flag; S.land_flag = 0; S.dirty |= D_LAND; }
     if (tp.dr) {
-      U4 d = draw(a.seed, gid, a.step, RNG_DR);
-      dr_m = uniform_f32(d.x, c.dr_lo, c.dr_hi);
-      dr_i = uniform_f32(d.y, c.dr_lo, c.dr_hi);
-      dr_t = uniform_f32(d.z, c.dr_lo, c.dr_hi);
-      st(a, OUZ_F_DR, i, dr_m); st(a, OUZ_F_DR + 1, i, dr_i); st(a, OUZ_F_DR + 2, i, dr_t);
+      U4 d = draw(a.seed, gid, sc.step, RNG_DR);
+      S.dr_m = uniform_f32(d.x, c.dr_lo, c.dr_hi);
+      S.dr_i = uniform_f32(d.y, c.dr_lo, c.dr_hi);
+      S.dr_t = uniform_f32(d.z, c.dr_lo, c.dr_hi);
+      S.dirty |= D_DR;
     }
-    if (tp.fault) {
-      U4 d = draw(a.seed, gid, a.step, RNG_FAULT);
-      sti(a, OUZ_I_FAULT_ROTOR, i, (int32_t)(d.x >> 30));
-      st(a, OUZ_F_FAULT_ETA, i, uniform_f32(d.y, 0.0f, c.fault_eta_hi));
-      sti(a, OUZ_I_FAULT_ONSET, i, (int32_t)(d.z % (uint32_t)(tp.max_ep / 2 + 1)));
+    if constexpr (CTRL == CTRL_RL) {
+      if (tp.fault) {
+        U4 d = draw(a.seed, gid, sc.step, RNG_FAULT);
+        S.frot = (int32_t)(d.x >> 30);
+        S.eta = uniform_f32(d.y, 0.0f, c.fault_eta_hi);
+        S.fonset = (int32_t)(d.z % (uint32_t)(tp.max_ep / 2 + 1));
+        S.dirty |= D_FAULT;
+      }
     }
   }
 
@@ -204,25 +317,23 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
 
   if constexpr (CTRL == CTRL_RL) {
     // ---- RL per-rotor thrust model (ouzelum.py:218-251) ----
-    if ((progress % 500) == 0 || rst) {   // set_targets (ouzelum.py:180-190)
-      U4 r = draw(a.seed, gid, a.step, RNG_TARGET);
+    if ((S.progress % 500) == 0 || rst) {   // set_targets (ouzelum.py:180-190)
+      U4 r = draw(a.seed, gid, sc.step, RNG_TARGET);
       target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
                   __fadd_rn(unit_f32(r.z), 1.0f));
     }
-    float4 act = reinterpret_cast<const float4*>(a.actions)[i];
+    float4 act = reinterpret_cast<const float4*>(sc.actions)[i];
     float av[4] = {act.x, act.y, act.z, act.w};
     float eff[4];
-    const bool on = tp.fault && progress >= ldi(a, OUZ_I_FAULT_ONSET, i);
-    const int frot = tp.fault ? ldi(a, OUZ_I_FAULT_ROTOR, i) : -1;
-    const float eta = tp.fault ? ld(a, OUZ_F_FAULT_ETA, i) : 1.0f;
+    const bool on = tp.fault && S.progress >= S.fonset;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float ak = fminf(fmaxf(av[k], -1.0f), 1.0f);                 // vec_task.py:327
-      float th = ld(a, OUZ_F_THRUST + k, i) + c.thrust_step * ak;
+      float th = S.thrust[k] + c.thrust_step * ak;
       th = fminf(fmaxf(th, 0.0f), c.thrust_max);                   // tensor_clamp
-      eff[k] = (on && frot == k) ? th * eta : th;
+      eff[k] = (on && S.frot == k) ? th * S.eta : th;
       if (rst) { th = 0.0f; eff[k] = 0.0f; }                        // thrusts/forces[reset] = 0
-      st(a, OUZ_F_THRUST + k, i, th);
+      S.thrust[k] = th;
     }
     float tot = 0.0f, tx = 0.0f, ty = 0.0f, tz = 0.0f;
 #pragma unroll
@@ -239,219 +350,258 @@ __device__ __forceinline__ void env_step(const StepArgs& a, int i, uint32_t gid,
     float T;
     V3 tau;
     const V3 cmd = v3(0.0f, 0.0f, 1.0f);
-    lee_position(p, q, v, w, cmd, 0.0f, default_gains(), T, tau);
+    lee_position(S.p, S.q, S.v, S.w, cmd, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
-    V3 dd = cmd - p;
+    V3 dd = cmd - S.p;
     if (sqrtf(dot(dd, dd)) < tp.land_radius) {
-      sti(a, OUZ_I_LAND_FLAG, i, 1);
+      S.land_flag = 1;
+      S.dirty |= D_LAND;
       fz = 0.0f;
       tau = v3(0.0f, 0.0f, 0.0f);
     }
     if (rst) fz = 0.0f;                        // forces[reset] = 0, torques kept
-    f_b = v3(0.0f, 0.0f, fz * dr_t);
+    f_b = v3(0.0f, 0.0f, fz * S.dr_t);
     tau_b = tau;
   } else {
     // ---- AHRS-EKF + PV-KF + waypoint guidance + Lee (ekf_lee_landed.py:308-530) ----
-    const bool conv = a.step < (uint32_t)c.conv_time;
+    const bool conv = sc.step < (uint32_t)c.conv_time;
     if constexpr (TGT == TGT_TRAJ) {
       // kinematic stand-in for the husky waypoint follower (landing.py:319-364)
-      int ttype = ldi(a, OUZ_I_TRAJ_TYPE, i), tidx = ldi(a, OUZ_I_TRAJ_IDX, i);
-      float sd = ld(a, OUZ_F_TRAJ_SD, i);
-      float2 pl = make_float2(ld(a, OUZ_F_PLAT, i), ld(a, OUZ_F_PLAT + 1, i));
-      if (a.step != 0) { target.x = pl.x + tp.plat_off_x; target.y = pl.y; }
-      float2 wpp = traj_point(a, ttype, tidx, sd);
-      float dx = wpp.x - pl.x, dy = wpp.y - pl.y;
-      if (sqrtf(dx * dx + dy * dy) < 0.2f) tidx += 1;
-      int len = ttype == 0 ? kTrajLen[0] : (ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
-      if (tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
-        U4 r = draw(a.seed, gid, a.step, RNG_TRAJ);
-        ttype = (int)(r.x % 3u);
-        sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
-        tidx = 0;
-        sti(a, OUZ_I_TRAJ_TYPE, i, ttype);
-        st(a, OUZ_F_TRAJ_SD, i, sd);
+      float2 wpp = traj_point(a, S.ttype, S.tidx, S.sd);
+      float dx = wpp.x - S.plat.x, dy = wpp.y - S.plat.y;
+      if (sqrtf(dx * dx + dy * dy) < 0.2f) S.tidx += 1;
+      int len = S.ttype == 0 ? kTrajLen[0] : (S.ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
+      if (S.tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
+        U4 r = draw(a.seed, gid, sc.step, RNG_TRAJ);
+        S.ttype = (int)(r.x % 3u);
+        S.sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
+        S.tidx = 0;
+        S.dirty |= D_TRAJ;
       }
-      sti(a, OUZ_I_TRAJ_IDX, i, tidx);
-      wpp = traj_point(a, ttype, tidx, sd);
-      dx = wpp.x - pl.x; dy = wpp.y - pl.y;
+      wpp = traj_point(a, S.ttype, S.tidx, S.sd);
+      dx = wpp.x - S.plat.x; dy = wpp.y - S.plat.y;
       float d = sqrtf(dx * dx + dy * dy);
       if (d > 0.0f) {
         float s = fminf(c.plat_speed * c.dt, d) / d;
-        pl.x += dx * s; pl.y += dy * s;
+        S.plat.x += dx * s; S.plat.y += dy * s;
       }
-      st(a, OUZ_F_PLAT, i, pl.x); st(a, OUZ_F_PLAT + 1, i, pl.y);
-      plat = pl;
     }
-    V3 prev_v = ld3(a, OUZ_F_PREV_V, i);
-    V3 lin_acc = v3((v.x - prev_v.x) / c.dt, (v.y - prev_v.y) / c.dt, (v.z - prev_v.z) / c.dt);
+    V3 lin_acc = v3((S.v.x - S.prev_v.x) / c.dt, (S.v.y - S.prev_v.y) / c.dt, (S.v.z - S.prev_v.z) / c.dt);
     lin_acc.z += 9.8f;                                 // aliasing quirk (ekf_lee_landed.py:366-367)
-    EkfQ qt{q.w, q.x, q.y, q.z};
-    EkfQ eq{ld(a, OUZ_F_EKF_Q, i), ld(a, OUZ_F_EKF_Q + 1, i), ld(a, OUZ_F_EKF_Q + 2, i), ld(a, OUZ_F_EKF_Q + 3, i)};
-    if (conv || rst) eq = qt;                          // :349-353
-    float px[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) px[k] = ld(a, OUZ_F_PV_X + k, i);
-    if (rst) { px[0] = p.x; px[1] = p.y; px[2] = p.z; px[3] = v.x; px[4] = v.y; px[5] = v.z; px[6] = px[7] = px[8] = 0.0f; }
-    float gyr[3] = {w.x, w.y, w.z};
+    EkfQ qt{S.q.w, S.q.x, S.q.y, S.q.z};
+    if (conv || rst) S.eq = qt;                        // :349-353
+    if (rst) {                                         // :355-360
+      S.px[0] = S.p.x; S.px[1] = S.p.y; S.px[2] = S.p.z; S.px[3] = S.v.x; S.px[4] = S.v.y; S.px[5] = S.v.z;
+      S.px[6] = S.px[7] = S.px[8] = 0.0f;
+    }
+    float gyr[3] = {S.w.x, S.w.y, S.w.z};
     float ang[4] = {qt.w, qt.x, qt.y, qt.z};
     if (!conv) {
-      pomdp_apply<3>(gyr, tp, task, a, gid, SITE_GYR, false);
-      pomdp_apply<4>(ang, tp, task, a, gid, SITE_ANG, true);
+      pomdp_apply<3>(gyr, tp, task, a, sc, gid, SITE_GYR, false);
+      pomdp_apply<4>(ang, tp, task, a, sc, gid, SITE_ANG, true);
     }
-    float eP[10];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) eP[k] = ld(a, OUZ_F_EKF_P + k, i);
     {
-      float inv = 1.0f / sqrtf(eq.w * eq.w + eq.x * eq.x + eq.y * eq.y + eq.z * eq.z);
-      eq = EkfQ{eq.w * inv, eq.x * inv, eq.y * inv, eq.z * inv};
+      float inv = 1.0f / sqrtf(S.eq.w * S.eq.w + S.eq.x * S.eq.x + S.eq.y * S.eq.y + S.eq.z * S.eq.z);
+      S.eq = EkfQ{S.eq.w * inv, S.eq.x * inv, S.eq.y * inv, S.eq.z * inv};
     }
-    ekf_update(eq, eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
-#pragma unroll
-    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, eP[k]);
-    st(a, OUZ_F_EKF_Q, i, eq.w); st(a, OUZ_F_EKF_Q + 1, i, eq.x); st(a, OUZ_F_EKF_Q + 2, i, eq.y); st(a, OUZ_F_EKF_Q + 3, i, eq.z);
-    // Phase fence: keeps the scheduler from hoisting the 45 PV-covariance loads above the EKF
-    // (it would otherwise hold ~100 state floats live across every phase: 408 registers, 1 wave/SIMD).
-    OUZ_SCHED_FENCE();
-    EkfQ orient = eq;
-    float pm[3] = {p.x, p.y, p.z}, vm[3] = {v.x, v.y, v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
+    ekf_update(S.eq, S.eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
+    EkfQ orient = S.eq;
+    float pm[3] = {S.p.x, S.p.y, S.p.z}, vm[3] = {S.v.x, S.v.y, S.v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
     if (conv) {
       orient = qt;
     } else {
-      pomdp_apply<3>(am, tp, task, a, gid, SITE_ACC, false);
-      pomdp_apply<3>(pm, tp, task, a, gid, SITE_POS, false);
-      pomdp_apply<3>(vm, tp, task, a, gid, SITE_VEL, false);
+      pomdp_apply<3>(am, tp, task, a, sc, gid, SITE_ACC, false);
+      pomdp_apply<3>(pm, tp, task, a, sc, gid, SITE_POS, false);
+      pomdp_apply<3>(vm, tp, task, a, sc, gid, SITE_VEL, false);
     }
-    float pP[45];
-#pragma unroll
-    for (int k = 0; k < 45; ++k) pP[k] = ld(a, OUZ_F_PV_P + k, i);
-    pv_predict(px, pP, v3(am[0], am[1], am[2]), orient, c.dt);
-    const uint64_t g = (uint64_t)a.step * a.n_total + gid;   // shared trigger counters (:425-440)
-    if (g % 7u == 6u) pv_correct<0>(px, pP, v3(pm[0], pm[1], pm[2]), kPvPosVar);
-    if (g % 3u == 0u) pv_correct<1>(px, pP, v3(vm[0], vm[1], vm[2]), 0.0f);   // R = 0 (PVFilter.py:76-79)
-    st3(a, OUZ_F_PREV_V, i, v);
-#pragma unroll
-    for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_X + k, i, px[k]);
-#pragma unroll
-    for (int k = 0; k < 45; ++k) st(a, OUZ_F_PV_P + k, i, pP[k]);
-    OUZ_SCHED_FENCE();
+    pv_predict(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt);
+    const uint64_t g = (uint64_t)sc.step * a.n_total + gid;   // shared trigger counters (:425-440)
+    if (g % 7u == 6u) pv_correct<0>(S.px, S.pP, v3(pm[0], pm[1], pm[2]), kPvPosVar);
+    if (g % 3u == 0u) pv_correct<1>(S.px, S.pP, v3(vm[0], vm[1], vm[2]), 0.0f);   // R = 0 (PVFilter.py:76-79)
+    S.prev_v = S.v;                                    // :454
     // waypoint guidance (:464-492)
-    V3 wp = conv ? target : ld3(a, OUZ_F_WAYPOINT, i);
-    V3 tv = target - p;
+    V3 wp = conv ? target : S.wp;
+    V3 tv = target - S.p;
     float td = sqrtf(dot(tv, tv));
     if (!conv) {
-      V3 wv = wp - p;
+      V3 wv = wp - S.p;
       float wd = sqrtf(dot(wv, wv));
       if (wd < 0.5f || wd > 1.0f) {
-        V3 vec = (target + v3(0.0f, 0.0f, 0.7f)) - p;
+        V3 vec = (target + v3(0.0f, 0.0f, 0.7f)) - S.p;
         float nv = sqrtf(dot(vec, vec));
-        wp = v3(vec.x / nv * 0.75f + p.x, vec.y / nv * 0.75f + p.y, vec.z / nv * 0.75f + p.z);
+        wp = v3(vec.x / nv * 0.75f + S.p.x, vec.y / nv * 0.75f + S.p.y, vec.z / nv * 0.75f + S.p.z);
       }
       if (td < 0.75f) wp = target + v3(0.0f, 0.0f, 0.09f);
     }
-    st3(a, OUZ_F_WAYPOINT, i, wp);
+    S.wp = wp;
     float T;
     V3 tau;
-    if (conv) lee_position(p, q, v, w, wp, 0.0f, default_gains(), T, tau);
-    else lee_position(v3(px[0], px[1], px[2]), q, v3(px[3], px[4], px[5]), w, wp, 0.0f, default_gains(), T, tau);
+    if (conv) lee_position(S.p, S.q, S.v, S.w, wp, 0.0f, default_gains(), T, tau);
+    else lee_position(v3(S.px[0], S.px[1], S.px[2]), S.q, v3(S.px[3], S.px[4], S.px[5]), S.w, wp, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
     if (td < tp.land_radius) {                       // :508-515
-      if (!conv) sti(a, OUZ_I_LAND_FLAG, i, 1);
+      if (!conv) { S.land_flag = 1; S.dirty |= D_LAND; }
       fz = 0.0f;
       tau = v3(0.0f, 0.0f, 0.0f);
     }
     if (rst) fz = 0.0f;                              // :521
     if (conv) { fz = 2.09f * kGravity; tau = v3(0.0f, 0.0f, 0.0f); }   // :526-530
-    f_b = v3(0.0f, 0.0f, fz * dr_t);
+    f_b = v3(0.0f, 0.0f, fz * S.dr_t);
     tau_b = tau;
   }
 
   // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
   {
-    const V3 I = v3(c.ixx * dr_i, c.iyy * dr_i, c.izz * dr_i);
-    const float inv_m = tp.dr ? 1.0f / (c.mass * dr_m) : c.inv_mass;
+    const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
+    const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
-    integrate(p, q, v, w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax);
+    integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax);
   }
 
   // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
-  progress += 1;
-  if constexpr (TGT == TGT_PLATFORM || TGT == TGT_TRAJ) {
-    target.x = plat.x + tp.plat_off_x;
-    target.y = plat.y;
+  S.progress += 1;
+  if constexpr (TGT == TGT_GOAL) {
+    S.target = target;
+  } else {
+    target.x = S.plat.x + tp.plat_off_x;
+    target.y = S.plat.y;
+    target.z = 0.377f;
   }
+  const V3 p = S.p, v = S.v, w = S.w;
+  const Q4 q = S.q;
   ob[0] = (target.x - p.x) / 3.0f; ob[1] = (target.y - p.y) / 3.0f; ob[2] = (target.z - p.z) / 3.0f;
   ob[3] = q.x; ob[4] = q.y; ob[5] = q.z; ob[6] = q.w;
   ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
   ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
-  pomdp_apply<13>(ob, tp, task, a, gid, SITE_OBS, false);
+  pomdp_apply<13>(ob, tp, task, a, sc, gid, SITE_OBS, false);
 #pragma unroll
   for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
-  float r = reward(p, target, q, w, dist);
-  const bool timeout_len = progress >= tp.max_ep - 1;
+  rew = reward(p, target, q, w, dist);
+  const bool timeout_len = S.progress >= tp.max_ep - 1;
   const bool die = dist > 8.0f || p.z < tp.z_die;
-  const bool rs = timeout_len || die;
-
-  // ---- stores ----
-  st3(a, OUZ_F_P, i, p);
-  st(a, OUZ_F_Q, i, q.x); st(a, OUZ_F_Q + 1, i, q.y); st(a, OUZ_F_Q + 2, i, q.z); st(a, OUZ_F_Q + 3, i, q.w);
-  st3(a, OUZ_F_V, i, v);
-  st3(a, OUZ_F_W, i, w);
-  if constexpr (TGT == TGT_GOAL) st3(a, OUZ_F_TARGET, i, target);
-  sti(a, OUZ_I_PROGRESS, i, progress);
-  a.rew[i] = r;
+  rs = timeout_len || die;
+  timeout = timeout_len && rs;                                             // vec_task.py:345
   if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
-    float er = ld(a, OUZ_F_EP_RET, i) + r;
-    if (rs) {
-      st(a, OUZ_F_EP_SUM, i, ld(a, OUZ_F_EP_SUM, i) + er);
-      sti(a, OUZ_I_EP_CNT, i, ldi(a, OUZ_I_EP_CNT, i) + 1);
-      er = 0.0f;
-    }
-    st(a, OUZ_F_EP_RET, i, er);
+    S.ep_ret += rew;
+    if (rs) { S.ep_sum_add += S.ep_ret; S.ep_cnt_add += 1; S.ep_ret = 0.0f; }
   }
-  a.reset[i] = rs ? 1 : 0;
-  a.timeouts[i] = (timeout_len && rs) ? 1 : 0;                             // vec_task.py:345
+  S.rst = rs;
 }
 
+// ---------------------------------------------------------------------------
+// Per-step outputs.  obs is (N, 13) AoS for the learners (vec_task.py:254-258): each wave stages
+// its 64 x 13 floats in LDS (lane stride 13 dwords: conflict-free) and writes its contiguous
+// 3328-byte slice with 16-byte stores instead of 13 strided dword stores per lane.  Staging is
+// wave-local, so waves of one block may run different task paths (mixed curriculum).
+// ---------------------------------------------------------------------------
 constexpr int kMaxBlock = 256;
 
-template <int TASK>
-__global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a) {
-  // obs is (N, 13) AoS for the learners (vec_task.py:254-258).  A lane's 13 floats are staged
-  // through LDS (stride 13 dwords: conflict-free) and the block writes its contiguous
-  // 52*blockDim-byte slice with 16-byte stores instead of 13 strided dword stores per lane.
-  __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
-  float* s_obs = reinterpret_cast<float*>(s_obs4);
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool valid = i < a.n;
-  float ob[OUZ_NUM_OBS];
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+struct OutPtrs {
+  float* obs;
+  float* rew;
+  int64_t* reset;
+  uint8_t* timeouts;
+};
+
+__device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, int n, bool valid, const float* ob,
+                                     float rew, bool rs, bool to) {
+  const int lane = threadIdx.x & 63;
+  const int first = i - lane;
   if (valid) {
-    const uint32_t gid = a.env_offset + (uint32_t)i;
-    if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-      env_step<CTRL_RL, TGT_GOAL>(a, i, gid, TASK, ob);
-    } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-      env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, TASK, ob);
-    } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-      env_step<CTRL_LEE_EST, TGT_PLATFORM>(a, i, gid, TASK, ob);
-    } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-      env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, TASK, ob);
-    } else {
-      const int t = mixed_task(gid);   // wave-uniform: 64-env blocks
-      if (t == OUZ_TASK_LEE_LANDED) env_step<CTRL_LEE_TRUE, TGT_PLATFORM>(a, i, gid, t, ob);
-      else if (t == OUZ_TASK_TRACKING) env_step<CTRL_LEE_EST, TGT_TRAJ>(a, i, gid, t, ob);
-      else env_step<CTRL_RL, TGT_GOAL>(a, i, gid, t, ob);
-    }
 #pragma unroll
-    for (int k = 0; k < OUZ_NUM_OBS; ++k) s_obs[threadIdx.x * OUZ_NUM_OBS + k] = ob[k];
+    for (int k = 0; k < OUZ_NUM_OBS; ++k) wave_lds[lane * OUZ_NUM_OBS + k] = ob[k];
+    o.rew[i] = rew;
+    o.reset[i] = rs ? 1 : 0;
+    o.timeouts[i] = to ? 1 : 0;
   }
-  __syncthreads();
-  const int base = blockIdx.x * blockDim.x;
-  const int nvalid = min((int)blockDim.x, a.n - base);
-  const int nf = nvalid * OUZ_NUM_OBS;            // floats of this block's slice
-  float* dst = a.obs + (size_t)base * OUZ_NUM_OBS; // 16-B aligned: blockDim is a multiple of 64
-  float4* dst4 = reinterpret_cast<float4*>(dst);
-  for (int k = threadIdx.x; k < nf / 4; k += blockDim.x) dst4[k] = s_obs4[k];
-  for (int k = (nf / 4) * 4 + threadIdx.x; k < nf; k += blockDim.x) dst[k] = s_obs[k];
+  wave_lds_sync();
+  const int m = min(64, n - first);
+  const int nf = m * OUZ_NUM_OBS;
+  float* dst = o.obs + (size_t)first * OUZ_NUM_OBS;   // 16-B aligned: waves start at multiples of 64 envs
+  const float4* src4 = reinterpret_cast<const float4*>(wave_lds);
+  for (int k = lane; k < nf / 4; k += 64) reinterpret_cast<float4*>(dst)[k] = src4[k];
+  for (int k = (nf / 4) * 4 + lane; k < nf; k += 64) dst[k] = wave_lds[k];
+  wave_lds_sync();
+}
+
+// K steps of one env: load once, K x (step + emit), store once.  MULTI = false is the single
+// VecTask.step kernel (K = 1, no loop, no rollout storage) and keeps the register budget of one step.
+template <int CTRL, int TGT, bool MULTI>
+__device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
+                                        size_t out_stride, float* wave_lds, int i, bool valid, int task) {
+  const TaskParams& tp = a.tp[task];
+  const uint32_t gid = a.env_offset + (uint32_t)i;
+  EnvRegs<CTRL, TGT> S;
+  if (valid) env_load<CTRL, TGT>(a, i, tp, S);
+  if constexpr (!MULTI) {
+    float ob[OUZ_NUM_OBS];
+    float rew = 0.0f;
+    bool rs = false, to = false;
+    if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
+    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to);
+  } else {
+    for (int k = 0; k < K; ++k) {
+      float ob[OUZ_NUM_OBS];
+      float rew = 0.0f;
+      bool rs = false, to = false;
+      if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
+      OutPtrs o = outs[0];
+      if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
+        o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
+        o.rew += (size_t)k * out_stride;
+        o.reset += (size_t)k * out_stride;
+        o.timeouts += (size_t)k * out_stride;
+        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to);
+        if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to);
+      } else {
+        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to);
+      }
+    }
+  }
+  if (valid) env_store<CTRL, TGT>(a, i, tp, S);
+}
+
+constexpr int kMaxRolloutChunk = 32;
+
+struct RolloutArgs {
+  int32_t K;
+  OutPtrs outs[2];          // [0] per-step target (env buffers or rollout storage), [1] env buffers
+  uint64_t out_stride;      // 0: write every step to outs[0]; else rollout storage with this env stride
+  StepCtx ctx[kMaxRolloutChunk];
+};
+
+template <int TASK, bool MULTI>
+__global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, RolloutArgs r) {
+  __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
+  float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int first = i - (int)(threadIdx.x & 63);
+  if (first >= a.n) return;                 // whole wave past the end
+  const bool valid = i < a.n;
+  if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
+    run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
+    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
+    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+  } else if constexpr (TASK == OUZ_TASK_TRACKING) {
+    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+  } else {
+    const int t = mixed_task(a.env_offset + (uint32_t)first);   // wave-uniform: 64-env blocks
+    if (t == OUZ_TASK_LEE_LANDED)
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
+    else if (t == OUZ_TASK_TRACKING)
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
+    else
+      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
+  }
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
@@ -781,7 +931,7 @@ int ouz_init_state(ouz_env* env, void* stream) {
 
 // Whole-batch flicker coins (utils/POMDP.py:25: one torch.rand(1) per call) — identical for
 // every env, so they are drawn once per step here instead of once per lane.
-static uint32_t flicker_mask(const StepArgs& a, int cfg_task) {
+static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
   uint32_t m = 0;
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
     if (cfg_task != OUZ_TASK_MIXED && t != cfg_task) continue;
@@ -789,50 +939,98 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task) {
     if (tp.pomdp != OUZ_POMDP_FLICKER && tp.pomdp != OUZ_POMDP_FLICKER_NOISE) continue;
     const float p = tp.pomdp == OUZ_POMDP_FLICKER ? tp.pomdp_prob : 0.1f;
     for (uint32_t site = 0; site < 6; ++site) {
-      U4 r = draw(a.seed, BATCH_ENV, a.step, RNG_POMDP + site, (uint32_t)t);
+      U4 r = draw(a.seed, BATCH_ENV, step, RNG_POMDP + site, (uint32_t)t);
       if (unit_f32(r.x) <= p) m |= 1u << (t * 8 + site);
     }
   }
   return m;
 }
 
-static int launch_step(ouz_env* env, const float* actions, hipStream_t s) {
-  StepArgs& a = env->args;
-  a.actions = actions;
-  a.step = (uint32_t)env->step;
-  a.flick_mask = flicker_mask(a, env->cfg.task);
+// Launch K (<= kMaxRolloutChunk) consecutive steps as ONE kernel.  K = 1 is VecTask.step.
+// ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
+// storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
+static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64_t ring_pos, int32_t K,
+                        const OutPtrs* storage, hipStream_t s) {
+  const StepArgs& a = env->args;
   const int n = env->cfg.num_envs, blk = block_for(n);
-  dim3 g(grid_for(n, blk)), b(blk);
-  switch (env->cfg.task) {
-    case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a); break;
-    case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a); break;
-    case OUZ_TASK_EKF_LEE_LANDED: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_EKF_LEE_LANDED>, g, b, 0, s, a); break;
-    case OUZ_TASK_TRACKING: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_TRACKING>, g, b, 0, s, a); break;
-    case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a); break;
-    default: hipLaunchKernelGGL(quad_step_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a); break;
+  RolloutArgs r;
+  std::memset(&r, 0, sizeof(r));
+  r.K = K;
+  const OutPtrs envout{env->buf.obs, env->buf.rew, env->buf.reset, env->buf.timeouts};
+  r.outs[0] = storage ? *storage : envout;
+  r.outs[1] = envout;
+  r.out_stride = storage ? (uint64_t)n : 0;
+  for (int k = 0; k < K; ++k) {
+    const uint32_t step = (uint32_t)(env->step + k);
+    r.ctx[k].step = step;
+    r.ctx[k].flick_mask = flicker_mask(a, env->cfg.task, step);
+    r.ctx[k].actions = ring ? ring + (size_t)((ring_pos + k) % ring_len) * n * OUZ_NUM_ACT : nullptr;
   }
+  dim3 g(grid_for(n, blk)), b(blk);
+#define OUZ_LAUNCH_TASK(T)                                         \
+  do {                                                             \
+    if (K == 1 && !storage) {                                      \
+      auto kfn = quad_step_kernel<T, false>;                       \
+      hipLaunchKernelGGL(kfn, g, b, 0, s, a, r);                   \
+    } else {                                                       \
+      auto kfn = quad_step_kernel<T, true>;                        \
+      hipLaunchKernelGGL(kfn, g, b, 0, s, a, r);                   \
+    }                                                              \
+  } while (0)
+  switch (env->cfg.task) {
+    case OUZ_TASK_OUZELUM: OUZ_LAUNCH_TASK(OUZ_TASK_OUZELUM); break;
+    case OUZ_TASK_LEE_LANDED: OUZ_LAUNCH_TASK(OUZ_TASK_LEE_LANDED); break;
+    case OUZ_TASK_EKF_LEE_LANDED: OUZ_LAUNCH_TASK(OUZ_TASK_EKF_LEE_LANDED); break;
+    case OUZ_TASK_TRACKING: OUZ_LAUNCH_TASK(OUZ_TASK_TRACKING); break;
+    case OUZ_TASK_FAULT: OUZ_LAUNCH_TASK(OUZ_TASK_FAULT); break;
+    default: OUZ_LAUNCH_TASK(OUZ_TASK_MIXED); break;
+  }
+#undef OUZ_LAUNCH_TASK
   OUZ_LAUNCH_CHECK("quad_step_kernel");
-  env->step += 1;
+  env->step += K;
   return OUZ_OK;
 }
 
 static bool needs_actions(int task) { return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_MIXED; }
 
+static int check_ring(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, const char* fn) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, std::string(fn) + ": env not bound");
+  if (n_steps < 0 || (ring && ring_len <= 0)) return fail(OUZ_ERR_INVALID, std::string(fn) + ": bad sizes");
+  if (!ring && needs_actions(env->cfg.task)) return fail(OUZ_ERR_INVALID, std::string(fn) + ": this task needs actions");
+  if (ring && (reinterpret_cast<uintptr_t>(ring) & 15u)) return fail(OUZ_ERR_INVALID, std::string(fn) + ": actions must be 16-byte aligned");
+  return OUZ_OK;
+}
+
 int ouz_step(ouz_env* env, const float* actions, void* stream) {
-  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_step: env not bound");
-  if (!actions && needs_actions(env->cfg.task)) return fail(OUZ_ERR_INVALID, "ouz_step: this task needs actions");
-  if (actions && (reinterpret_cast<uintptr_t>(actions) & 15u)) return fail(OUZ_ERR_INVALID, "ouz_step: actions must be 16-byte aligned");
-  return launch_step(env, actions, (hipStream_t)stream);
+  int rc = check_ring(env, actions, 1, 1, "ouz_step");
+  if (rc) return rc;
+  return launch_steps(env, actions, 1, 0, 1, nullptr, (hipStream_t)stream);
 }
 
 int ouz_step_n(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, void* stream) {
-  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_step_n: env not bound");
-  if (n_steps < 0 || (ring && ring_len <= 0)) return fail(OUZ_ERR_INVALID, "ouz_step_n: bad sizes");
-  if (!ring && needs_actions(env->cfg.task)) return fail(OUZ_ERR_INVALID, "ouz_step_n: this task needs actions");
+  int rc = check_ring(env, ring, ring_len, n_steps, "ouz_step_n");
+  if (rc) return rc;
   for (int32_t k = 0; k < n_steps; ++k) {
-    const float* act = ring ? ring + (size_t)(k % ring_len) * env->cfg.num_envs * OUZ_NUM_ACT : nullptr;
-    int r = launch_step(env, act, (hipStream_t)stream);
-    if (r) return r;
+    rc = launch_steps(env, ring, ring_len, k, 1, nullptr, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return OUZ_OK;
+}
+
+int ouz_rollout(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out, float* rew_out,
+                int64_t* reset_out, uint8_t* timeouts_out, void* stream) {
+  int rc = check_ring(env, ring, ring_len, n_steps, "ouz_rollout");
+  if (rc) return rc;
+  const bool store = obs_out || rew_out || reset_out || timeouts_out;
+  if (store && !(obs_out && rew_out && reset_out && timeouts_out))
+    return fail(OUZ_ERR_INVALID, "ouz_rollout: give all four storage pointers or none");
+  const size_t n = (size_t)env->cfg.num_envs;
+  for (int32_t k0 = 0; k0 < n_steps; k0 += kMaxRolloutChunk) {
+    const int32_t K = (n_steps - k0) < kMaxRolloutChunk ? (n_steps - k0) : kMaxRolloutChunk;
+    OutPtrs st{obs_out + (size_t)k0 * n * OUZ_NUM_OBS, rew_out + (size_t)k0 * n, reset_out + (size_t)k0 * n,
+               timeouts_out + (size_t)k0 * n};
+    rc = launch_steps(env, ring, ring_len, k0, K, store ? &st : nullptr, (hipStream_t)stream);
+    if (rc) return rc;
   }
   return OUZ_OK;
 }

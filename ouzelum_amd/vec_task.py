@@ -235,18 +235,42 @@ class QuadVecTask:
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
 
-    def rollout(self, action_ring, n_steps):
-        """``n_steps`` consecutive steps over a ring of pre-staged action batches (T, N, 4)
-        with one C call (the train_vec.py env-only loop without Python in between)."""
+    def rollout(self, action_ring, n_steps, fused=False, storage=None):
+        """``n_steps`` consecutive VecTask.step calls over a ring of pre-staged action batches
+        ``(T, N, 4)`` (``None`` for the Lee tasks, which ignore actions) with one C call.
+
+        ``fused=False``: one kernel launch per step (``ouz_step_n``).  ``fused=True``: up to 32
+        steps per launch with the env state held in registers (``ouz_rollout``); with
+        ``storage=(obs (K,N,13), rew (K,N), reset (K,N) int64, time_outs (K,N) bool)`` every
+        step's outputs land in the learner's rollout buffers, the env buffers keep the last step.
+        """
         if action_ring is None:
-            L.check(L.lib.ouz_step_n(self._env, L.ptr(self._zero_actions), 1, int(n_steps), self._stream()),
-                    "ouz_step_n")
+            ring_ptr, ring_len = None, 1
+            if self.uses_actions:
+                ring_ptr = L.ptr(self._zero_actions)
+        else:
+            L.require_hip_tensor(action_ring, "action_ring")
+            if action_ring.dim() != 3 or action_ring.shape[1:] != (self.num_envs, self.num_actions):
+                raise ValueError("action_ring must be (T, num_envs, 4)")
+            ring_ptr, ring_len = L.ptr(action_ring), action_ring.shape[0]
+        if not fused:
+            if storage is not None:
+                raise ValueError("storage needs fused=True")
+            L.check(L.lib.ouz_step_n(self._env, ring_ptr, ring_len, int(n_steps), self._stream()), "ouz_step_n")
             return
-        L.require_hip_tensor(action_ring, "action_ring")
-        if action_ring.dim() != 3 or action_ring.shape[1:] != (self.num_envs, self.num_actions):
-            raise ValueError("action_ring must be (T, num_envs, 4)")
-        L.check(L.lib.ouz_step_n(self._env, L.ptr(action_ring), action_ring.shape[0], int(n_steps),
-                                 self._stream()), "ouz_step_n")
+        ptrs = [None] * 4
+        if storage is not None:
+            obs, rew, rst, to = storage
+            n = self.num_envs
+            for tns, shape, dt, name in ((obs, (n_steps, n, 13), torch.float32, "obs"),
+                                         (rew, (n_steps, n), torch.float32, "rew"),
+                                         (rst, (n_steps, n), torch.int64, "reset"),
+                                         (to, (n_steps, n), torch.bool, "time_outs")):
+                L.require_hip_tensor(tns, name)
+                if tuple(tns.shape[:len(shape)]) != shape or tns.dtype != dt:
+                    raise ValueError(f"storage {name} must be {shape} {dt}")
+            ptrs = [L.ptr(obs), L.ptr(rew), L.ptr(rst), L.ptr(to)]
+        L.check(L.lib.ouz_rollout(self._env, ring_ptr, ring_len, int(n_steps), *ptrs, self._stream()), "ouz_rollout")
 
     def reset(self):
         """vec_task.py:377-389: returns the current obs, does not touch the simulation."""

@@ -212,3 +212,34 @@ def test_baseline_size_properties(ouz, task, n):
     assert bool((env.timeout_buf.long() <= env.reset_buf).all())
     qn = env.fstate[3:7].norm(dim=0)
     assert float((qn - 1).abs().max()) < 1e-5
+
+
+@pytest.mark.parametrize("task", TASKS)
+def test_fused_rollout_matches_single_steps(ouz, task):
+    """ouz_rollout (32 steps per launch, state in registers, outputs to rollout storage) gives the
+    same trajectory as 40 single-step launches."""
+    n, K = 2048, 40
+    kw = {"convergence_time": 12} if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else {}
+    a = ouz.make(seed=9, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True, **kw)
+    b = ouz.make(seed=9, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True, **kw)
+    g = torch.Generator(device="cuda").manual_seed(2)
+    ring = (torch.rand((7, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
+    obs_s = torch.empty((K, n, 13), device="cuda")
+    rew_s = torch.empty((K, n), device="cuda")
+    rst_s = torch.empty((K, n), dtype=torch.int64, device="cuda")
+    to_s = torch.empty((K, n), dtype=torch.bool, device="cuda")
+    a.rollout(ring, K, fused=True, storage=(obs_s, rew_s, rst_s, to_s))
+    obs_r, rew_r, rst_r = [], [], []
+    for k in range(K):
+        b.step(ring[k % 7])
+        obs_r.append(b.obs_buf.clone())
+        rew_r.append(b.rew_buf.clone())
+        rst_r.append(b.reset_buf.clone())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(obs_s, torch.stack(obs_r), atol=2e-5, rtol=1e-5)
+    torch.testing.assert_close(rew_s, torch.stack(rew_r), atol=2e-5, rtol=1e-5)
+    assert torch.equal(rst_s, torch.stack(rst_r))
+    torch.testing.assert_close(a.fstate, b.fstate, atol=5e-4, rtol=1e-4)
+    assert torch.equal(a.istate, b.istate)
+    assert torch.equal(a.reset_buf, b.reset_buf) and torch.equal(a.obs_buf, obs_s[-1])
+    assert a.sim_step_count == b.sim_step_count == K
