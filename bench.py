@@ -131,11 +131,13 @@ def cpu_baseline(task, n, seed, budget_s):
     o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=seed))
     rs = np.random.RandomState(0)
     acts = rs.uniform(-1, 1, (RING, n, 4))
-    t0 = time.perf_counter()
-    for k in range(3):
+    for k in range(3):                       # warm-up (first steps allocate)
         o.step(acts[k % RING])
-    per = (time.perf_counter() - t0) / 3
-    steps = int(max(5, min(2000, budget_s / max(per, 1e-6))))
+    t0 = time.perf_counter()
+    for k in range(5):
+        o.step(acts[k % RING])
+    per = (time.perf_counter() - t0) / 5
+    steps = int(max(5, min(20000, budget_s / max(per, 1e-6))))
     t0 = time.perf_counter()
     for k in range(steps):
         o.step(acts[k % RING])

@@ -31,6 +31,8 @@
  *   ouz_ekf_update  EKF.update (ang branch)    ahrs_ekf.py:1280-1337
  *   ouz_pv_predict  PVFilter.prediction_step   PVFilter.py:25-64
  *   ouz_pv_correct  PVFilter.correction_step   PVFilter.py:67-110
+ *   ouz_pv_step     the driver's per-env predict -> position fix -> velocity fix (ekf_lee_landed.py:417-444),
+ *                   evaluated in f64 with f32 storage, as inside ouz_step
  *   ouz_integrate   gym.simulate (PhysX)       tasks/base/vec_task.py:332-335 (build-defined integrator)
  *   ouz_reward      compute_ingenuity_reward   tasks/ekf_lee_landed.py:692-723
  *   ouz_philox      the counter RNG every draw of the step uses (replaces torch_rand_float /
@@ -182,6 +184,8 @@ int ouz_pv_predict(float* x9, float* P45, const float* acc, const float* q_wxyz,
                    void* stream);
 int ouz_pv_correct(float* x9, float* P45, const float* z, int32_t block, float var, const uint8_t* mask,
                    int32_t n, void* stream);
+int ouz_pv_step(float* x9, float* P45, const float* acc, const float* q_wxyz, float dt, const float* pos_z,
+                const uint8_t* pos_mask, const float* vel_z, const uint8_t* vel_mask, int32_t n, void* stream);
 int ouz_integrate(float* root13, const float* f_b, const float* tau_b, const float* mass, const float* inertia,
                   float dt, int32_t substeps, int32_t n, void* stream);
 int ouz_reward(const float* root13, const float* target, const int32_t* progress, int32_t max_episode_length,

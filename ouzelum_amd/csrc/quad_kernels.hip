@@ -414,10 +414,10 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       pomdp_apply<3>(pm, tp, task, a, sc, gid, SITE_POS, false);
       pomdp_apply<3>(vm, tp, task, a, sc, gid, SITE_VEL, false);
     }
-    pv_predict(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt);
-    const uint64_t g = (uint64_t)sc.step * a.n_total + gid;   // shared trigger counters (:425-440)
-    if (g % 7u == 6u) pv_correct<0>(S.px, S.pP, v3(pm[0], pm[1], pm[2]), kPvPosVar);
-    if (g % 3u == 0u) pv_correct<1>(S.px, S.pP, v3(vm[0], vm[1], vm[2]), 0.0f);   // R = 0 (PVFilter.py:76-79)
+    // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
+    const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
+    pv_step(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u,
+            v3(vm[0], vm[1], vm[2]));
     S.prev_v = S.v;                                    // :454
     // waypoint guidance (:464-492)
     V3 wp = conv ? target : S.wp;
@@ -708,6 +708,25 @@ __global__ void __launch_bounds__(64) pv_correct_kernel(float* x, float* P, cons
   #pragma unroll
   for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
   #pragma unroll
+  for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
+}
+
+__global__ void __launch_bounds__(64) pv_step_kernel(float* x, float* P, const float* acc, const float* q, float dt,
+                                                     const float* zp, const uint8_t* pmask, const float* zv,
+                                                     const uint8_t* vmask, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float xx[9], pp[45];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+#pragma unroll
+  for (int k = 0; k < 45; ++k) pp[k] = P[i * 45 + k];
+  pv_step(xx, pp, v3(acc[i * 3], acc[i * 3 + 1], acc[i * 3 + 2]), EkfQ{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]}, dt,
+          pmask && pmask[i], zp ? v3(zp[i * 3], zp[i * 3 + 1], zp[i * 3 + 2]) : v3(0, 0, 0), vmask && vmask[i],
+          zv ? v3(zv[i * 3], zv[i * 3 + 1], zv[i * 3 + 2]) : v3(0, 0, 0));
+#pragma unroll
+  for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+#pragma unroll
   for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
 }
 
@@ -1096,6 +1115,17 @@ int ouz_pv_correct(float* x, float* P, const float* z, int32_t block, float var,
   if (block != 0 && block != 1) return fail(OUZ_ERR_INVALID, "ouz_pv_correct: block must be 0 (position) or 1 (velocity)");
   hipLaunchKernelGGL(pv_correct_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, x, P, z, block, var, mask, n);
   OUZ_LAUNCH_CHECK("pv_correct_kernel");
+  return OUZ_OK;
+}
+
+int ouz_pv_step(float* x, float* P, const float* acc, const float* q, float dt, const float* pos_z,
+                const uint8_t* pos_mask, const float* vel_z, const uint8_t* vel_mask, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_pv_step");
+  if (!x || !P || !acc || !q) return fail(OUZ_ERR_INVALID, "ouz_pv_step: null pointer");
+  if ((pos_mask && !pos_z) || (vel_mask && !vel_z)) return fail(OUZ_ERR_INVALID, "ouz_pv_step: mask without data");
+  hipLaunchKernelGGL(pv_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, x, P, acc, q, dt, pos_z,
+                     pos_mask, vel_z, vel_mask, n);
+  OUZ_LAUNCH_CHECK("pv_step_kernel");
   return OUZ_OK;
 }
 

@@ -22,7 +22,9 @@ namespace ouz {
 // ---------------------------------------------------------------------------
 struct V3 { float x, y, z; };
 struct Q4 { float x, y, z, w; };          // xyzw (Isaac root-state order)
-struct M3 { float m[9]; };                 // row-major
+template <typename T>
+struct M3T { T m[9]; };                    // row-major
+using M3 = M3T<float>;
 
 OUZ_HD V3 v3(float x, float y, float z) { return V3{x, y, z}; }
 OUZ_HD V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
@@ -41,8 +43,15 @@ OUZ_HD V3 mtv(const M3& A, V3 v) {  // A^T v
   return V3{A.m[0] * v.x + A.m[3] * v.y + A.m[6] * v.z, A.m[1] * v.x + A.m[4] * v.y + A.m[7] * v.z,
             A.m[2] * v.x + A.m[5] * v.y + A.m[8] * v.z};
 }
-OUZ_HD M3 mm(const M3& A, const M3& B) {
-  M3 C;
+// A (3x3) times the 3-vector a[0..2], into out[0..2]
+template <typename T>
+OUZ_HD void mva(const M3T<T>& A, const T* a, T* out) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out[i] = A.m[i * 3 + 0] * a[0] + A.m[i * 3 + 1] * a[1] + A.m[i * 3 + 2] * a[2];
+}
+template <typename T>
+OUZ_HD M3T<T> mm(const M3T<T>& A, const M3T<T>& B) {
+  M3T<T> C;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -50,8 +59,9 @@ OUZ_HD M3 mm(const M3& A, const M3& B) {
       C.m[i * 3 + j] = A.m[i * 3 + 0] * B.m[0 * 3 + j] + A.m[i * 3 + 1] * B.m[1 * 3 + j] + A.m[i * 3 + 2] * B.m[2 * 3 + j];
   return C;
 }
-OUZ_HD M3 mmt(const M3& A, const M3& B) {  // A B^T
-  M3 C;
+template <typename T>
+OUZ_HD M3T<T> mmt(const M3T<T>& A, const M3T<T>& B) {  // A B^T
+  M3T<T> C;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -59,32 +69,37 @@ OUZ_HD M3 mmt(const M3& A, const M3& B) {  // A B^T
       C.m[i * 3 + j] = A.m[i * 3 + 0] * B.m[j * 3 + 0] + A.m[i * 3 + 1] * B.m[j * 3 + 1] + A.m[i * 3 + 2] * B.m[j * 3 + 2];
   return C;
 }
-OUZ_HD M3 tr(const M3& A) {
-  M3 C;
+template <typename T>
+OUZ_HD M3T<T> tr(const M3T<T>& A) {
+  M3T<T> C;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) C.m[i * 3 + j] = A.m[j * 3 + i];
   return C;
 }
-OUZ_HD M3 madd(const M3& A, const M3& B) { M3 C;
+template <typename T>
+OUZ_HD M3T<T> madd(const M3T<T>& A, const M3T<T>& B) { M3T<T> C;
 #pragma unroll
   for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] + B.m[k]; return C; }
-OUZ_HD M3 msub(const M3& A, const M3& B) { M3 C;
+template <typename T>
+OUZ_HD M3T<T> msub(const M3T<T>& A, const M3T<T>& B) { M3T<T> C;
 #pragma unroll
   for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] - B.m[k]; return C; }
-OUZ_HD M3 mscale(float s, const M3& A) { M3 C;
+template <typename T>
+OUZ_HD M3T<T> mscale(T s, const M3T<T>& A) { M3T<T> C;
 #pragma unroll
   for (int k = 0; k < 9; ++k) C.m[k] = s * A.m[k]; return C; }
 
 // Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).
-OUZ_HD M3 inv_sym3(const M3& S) {
-  float a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
-  float A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
-  float D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
-  float inv_det = 1.0f / (a * A + b * B + c * C);
-  return M3{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
-             C * inv_det, E * inv_det, F * inv_det}};
+template <typename T>
+OUZ_HD M3T<T> inv_sym3(const M3T<T>& S) {
+  T a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
+  T A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
+  T D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
+  T inv_det = T(1) / (a * A + b * B + c * C);
+  return M3T<T>{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
+                 C * inv_det, E * inv_det, F * inv_det}};
 }
 
 // ---------------------------------------------------------------------------
@@ -381,8 +396,9 @@ OUZ_HD constexpr int s9(int i, int j) {
 }
 
 // 3x3 block (bi, bj) of the packed 9x9 (bi, bj in 0..2).
-OUZ_HD M3 pblk(const float P[45], int bi, int bj) {
-  M3 B;
+template <typename T>
+OUZ_HD M3T<T> pblk(const T P[45], int bi, int bj) {
+  M3T<T> B;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -390,7 +406,8 @@ OUZ_HD M3 pblk(const float P[45], int bi, int bj) {
   return B;
 }
 // Store block (bi <= bj); for a diagonal block only its upper triangle is kept.
-OUZ_HD void pset(float P[45], int bi, int bj, const M3& B) {
+template <typename T>
+OUZ_HD void pset(T P[45], int bi, int bj, const M3T<T>& B) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -402,14 +419,6 @@ constexpr float kPvAccVar = 1.0f;     // [0.01]*3 * 100 (ekf_lee_landed.py:137)
 constexpr float kPvPosVar = 1e-7f;    // ekf_lee_landed.py:408
 constexpr float kPvP0 = 1000.0f;      // PVFilter.py:12
 
-// Scheduling fence between phases of one env's math: the AMDGPU scheduler otherwise
-// interleaves independent 3x3 block products and holds all their temporaries live.
-#if defined(__HIP_DEVICE_COMPILE__)
-#define OUZ_PHASE() ((void)0)
-#else
-#define OUZ_PHASE() ((void)0)
-#endif
-
 // prediction_step: M = R(q/|q|)^T; F = [[I, M dt, M h],[0, M, M dt],[0,0,I]], G = F[:, 6:9] (rows 0..5),
 // x = F x + G (a - b); P = F P F^T + q_a G G^T.   (h = dt^2/2)
 // Block form, P = [[A, B, C], [B^T, D, E], [C^T, E^T, Fb]]:
@@ -417,81 +426,131 @@ constexpr float kPvP0 = 1000.0f;      // PVFilter.py:12
 //   T23 = M (E + dt Fb)         T22 = M (D + dt E^T)
 //   A' = T11 + (dt T12 + h T13) M^T + q h^2 M M^T     B' = (T12 + dt T13) M^T + q h dt M M^T
 //   D' = (T22 + dt T23) M^T + q dt^2 M M^T             C' = T13, E' = T23, Fb' = Fb
-OUZ_HD void pv_predict(float x[9], float P[45], V3 acc, EkfQ q, float dt) {
+// M is formed in f32 from the f32 quaternion (as the reference's torch f32 does); the
+// covariance arithmetic runs in T.
+template <typename T>
+OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
   float inv = 1.0f / sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
-  const M3 M = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
-  const float h = dt * dt * 0.5f;
+  const M3 Mf = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
+  M3T<T> M;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) M.m[k] = (T)Mf.m[k];
+  const T h = dt * dt * T(0.5);
   {
-    V3 xp = v3(x[0], x[1], x[2]), xv = v3(x[3], x[4], x[5]), xb = v3(x[6], x[7], x[8]);
-    V3 u = acc - xb;
-    V3 np_ = xp + mv(M, dt * xv) + mv(M, h * xb) + mv(M, h * u);
-    V3 nv = mv(M, xv) + mv(M, dt * xb) + mv(M, dt * u);
-    x[0] = np_.x; x[1] = np_.y; x[2] = np_.z;
-    x[3] = nv.x; x[4] = nv.y; x[5] = nv.z;
+    T a1[3], a2[3], o[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      T u = acc[k] - x[6 + k];
+      a1[k] = dt * x[3 + k] + h * x[6 + k] + h * u;   // -> position
+      a2[k] = x[3 + k] + dt * x[6 + k] + dt * u;      // -> velocity
+    }
+    mva(M, a1, o);
+    x[0] += o[0]; x[1] += o[1]; x[2] += o[2];
+    mva(M, a2, o);
+    x[3] = o[0]; x[4] = o[1]; x[5] = o[2];
   }
-  const M3 MMt = mmt(M, M);
-  OUZ_PHASE();
-  M3 T13 = madd(pblk(P, 0, 2), mm(M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2)))));
-  OUZ_PHASE();
-  M3 T12 = madd(pblk(P, 0, 1), mm(M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1)))));
-  OUZ_PHASE();
+  const T q_a = (T)kPvAccVar;
+  const M3T<T> MMt = mmt(M, M);
+  M3T<T> T13 = madd(pblk(P, 0, 2), mm(M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2)))));
+  M3T<T> T12 = madd(pblk(P, 0, 1), mm(M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1)))));
   {
-    M3 T11 = madd(pblk(P, 0, 0), mm(M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0)))));
-    OUZ_PHASE();
-    pset(P, 0, 0, madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(kPvAccVar * h * h, MMt)));
+    M3T<T> T11 = madd(pblk(P, 0, 0), mm(M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0)))));
+    pset(P, 0, 0, madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(q_a * h * h, MMt)));
   }
-  OUZ_PHASE();
-  pset(P, 0, 1, madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(kPvAccVar * h * dt, MMt)));
-  OUZ_PHASE();
-  M3 T23 = mm(M, madd(pblk(P, 1, 2), mscale(dt, pblk(P, 2, 2))));
-  OUZ_PHASE();
-  M3 T22 = mm(M, madd(pblk(P, 1, 1), mscale(dt, pblk(P, 2, 1))));
-  OUZ_PHASE();
-  pset(P, 1, 1, madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(kPvAccVar * dt * dt, MMt)));
+  pset(P, 0, 1, madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(q_a * h * dt, MMt)));
+  M3T<T> T23 = mm(M, madd(pblk(P, 1, 2), mscale(dt, pblk(P, 2, 2))));
+  M3T<T> T22 = mm(M, madd(pblk(P, 1, 1), mscale(dt, pblk(P, 2, 1))));
+  pset(P, 1, 1, madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(q_a * dt * dt, MMt)));
   pset(P, 0, 2, T13);
   pset(P, 1, 2, T23);
-  OUZ_PHASE();
 }
 
 // correction_step for one measured block m (0 = position, 1 = velocity) with R = r I.
 // Stable form of x += K (z - x_m); P = (I - K H) P  (DESIGN.md §4):
 //   S = P_mm + r I;  K_o = P_om S^-1 (o != m)
 //   x_m = z - r S^-1 y;  x_o += K_o y
-//   P_mm = r (I - r S^-1);  P_mo = r S^-1 P_mo;  P_oo' = P_oo' - K_o P_mo'
-template <int MB>
-OUZ_HD void pv_correct(float x[9], float P[45], V3 z, float r) {
+//   P_mm = r (I - r S^-1);  P_mo = r S^-1 P_mo = r K_o^T;  P_oo' = P_oo' - K_o P_mo'
+template <int MB, typename T>
+OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
   constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
   constexpr int B = 2;
-  M3 Si;
+  M3T<T> Si;
   {
-    M3 S = pblk(P, MB, MB);
+    M3T<T> S = pblk(P, MB, MB);
     S.m[0] += r; S.m[4] += r; S.m[8] += r;
     Si = inv_sym3(S);
   }
-  OUZ_PHASE();
-  const M3 KA = mm(pblk(P, A, MB), Si), KB = mm(pblk(P, B, MB), Si);     // K_o = P_{o,m} S^-1
+  const M3T<T> KA = mm(pblk(P, A, MB), Si), KB = mm(pblk(P, B, MB), Si);     // K_o = P_{o,m} S^-1
   {
-    V3 y = z - v3(x[MB * 3 + 0], x[MB * 3 + 1], x[MB * 3 + 2]);
-    V3 nm = z - r * mv(Si, y);
-    V3 dA = mv(KA, y), dB = mv(KB, y);
-    x[MB * 3 + 0] = nm.x; x[MB * 3 + 1] = nm.y; x[MB * 3 + 2] = nm.z;
-    x[A * 3 + 0] += dA.x; x[A * 3 + 1] += dA.y; x[A * 3 + 2] += dA.z;
-    x[B * 3 + 0] += dB.x; x[B * 3 + 1] += dB.y; x[B * 3 + 2] += dB.z;
+    T y[3] = {z[0] - x[MB * 3 + 0], z[1] - x[MB * 3 + 1], z[2] - x[MB * 3 + 2]};
+    T sy[3], dA[3], dB[3];
+    mva(Si, y, sy);
+    mva(KA, y, dA);
+    mva(KB, y, dB);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      x[MB * 3 + k] = z[k] - r * sy[k];
+      x[A * 3 + k] += dA[k];
+      x[B * 3 + k] += dB[k];
+    }
   }
-  OUZ_PHASE();
   // other-other blocks first: they read P_{m,o}, which is overwritten below
   pset(P, B, B, msub(pblk(P, B, B), mm(KB, pblk(P, MB, B))));
-  OUZ_PHASE();
   pset(P, A, B, msub(pblk(P, A, B), mm(KA, pblk(P, MB, B))));
-  OUZ_PHASE();
   pset(P, A, A, msub(pblk(P, A, A), mm(KA, pblk(P, MB, A))));
-  OUZ_PHASE();
-  // P_{m,o} = r S^-1 P_{m,o} = r K_o^T
   if (MB < A) pset(P, MB, A, mscale(r, tr(KA))); else pset(P, A, MB, mscale(r, KA));
   pset(P, MB, B, mscale(r, tr(KB)));
-  M3 I3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+  M3T<T> I3{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
   pset(P, MB, MB, mscale(r, msub(I3, mscale(r, Si))));
-  OUZ_PHASE();
+}
+
+// One PV-filter step as the driver runs it (ekf_lee_landed.py:417-444): predict, then the
+// position fix if triggered, then the velocity fix (R = 0) if triggered.  The state and
+// covariance are STORED in f32 but the whole step is evaluated in PvReal: the covariance
+// carries ~10 decades between the R = 1e-7 fixed position and the O(1e3) bias directions,
+// and rounding it to f32 between predict and correct loses the bias information
+// (the reference's own f32 evaluation drifts by ~2x the state).
+typedef double PvReal;
+
+OUZ_HD void pv_step(float xf[9], float Pf[45], V3 acc, EkfQ q, float dt, bool pos_fix, V3 zp, bool vel_fix, V3 zv) {
+  PvReal x[9], P[45];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) x[k] = (PvReal)xf[k];
+#pragma unroll
+  for (int k = 0; k < 45; ++k) P[k] = (PvReal)Pf[k];
+  const PvReal a[3] = {(PvReal)acc.x, (PvReal)acc.y, (PvReal)acc.z};
+  pv_predict_t<PvReal>(x, P, a, q, (PvReal)dt);
+  if (pos_fix) {
+    const PvReal z[3] = {(PvReal)zp.x, (PvReal)zp.y, (PvReal)zp.z};
+    pv_correct_t<0, PvReal>(x, P, z, (PvReal)kPvPosVar);
+  }
+  if (vel_fix) {
+    const PvReal z[3] = {(PvReal)zv.x, (PvReal)zv.y, (PvReal)zv.z};
+    pv_correct_t<1, PvReal>(x, P, z, PvReal(0));
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) xf[k] = (float)x[k];
+#pragma unroll
+  for (int k = 0; k < 45; ++k) Pf[k] = (float)P[k];
+}
+
+// Single-call forms (PVFilter.prediction_step / correction_step) on f32 storage.
+OUZ_HD void pv_predict(float xf[9], float Pf[45], V3 acc, EkfQ q, float dt) {
+  pv_step(xf, Pf, acc, q, dt, false, acc, false, acc);
+}
+template <int MB>
+OUZ_HD void pv_correct(float xf[9], float Pf[45], V3 z, float r) {
+  PvReal x[9], P[45];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) x[k] = (PvReal)xf[k];
+#pragma unroll
+  for (int k = 0; k < 45; ++k) P[k] = (PvReal)Pf[k];
+  const PvReal zz[3] = {(PvReal)z.x, (PvReal)z.y, (PvReal)z.z};
+  pv_correct_t<MB, PvReal>(x, P, zz, (PvReal)r);
+#pragma unroll
+  for (int k = 0; k < 9; ++k) xf[k] = (float)x[k];
+#pragma unroll
+  for (int k = 0; k < 45; ++k) Pf[k] = (float)P[k];
 }
 
 // ---------------------------------------------------------------------------

@@ -95,21 +95,21 @@ def _relerr(a, b):
     return float((np.abs(a - b).max(1) / np.maximum(1.0, np.abs(b).max(1))).max())
 
 
+@pytest.mark.parametrize("separate", [False, True])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
+def test_pvfilter_sequence_vs_reference_golden(L, golden, seed, separate):
     """28 chained PV predict/correct steps with the shared trigger pattern (PVFilter.py:25-110).
 
     The golden inputs are adversarial (random position/velocity fixes every step, so the
     accelerometer-bias states run to O(100-1000) m/s^2).  With R = 1e-7 the bias is estimated
-    from ratios of covariance entries that are themselves differences of O(1e3) terms: the
-    reference's OWN float32 torch run (golden x_f32ref / P_f32ref) drifts from its float64 run
-    by up to ~2.4x the state magnitude and ~20 % of the covariance.  A float32 evaluation of the
-    stable form drifts too (CPU emulation: up to ~0.45 of the state; float64 arithmetic inside
-    the step with float32 storage would hold ~3e-4).  Requirements here:
-    (1) the first 6 steps (before the bias states blow up) agree with float64 to 1e-4;
-    (2) over the whole sequence it is at least 4x closer to float64 than the reference's f32 run.
-    Realistic-regime parity of the same device code is held to 2e-4 inside the fused step
-    (test_gpu_env.py::test_single_step_parity, EKF tasks).
+    from ratios of covariance entries that are differences of O(1e3) terms: the reference's OWN
+    float32 torch run (golden x_f32ref / P_f32ref) drifts from its float64 run by up to ~2.4x the
+    state magnitude and ~20 % of the covariance.  The HIP filter evaluates each step in float64
+    and stores float32.  Requirements:
+    * fused predict + fixes (ouz_pv_step, what ouz_step runs): within 1e-3 of float64 on every
+      step and >= 100x closer than the reference's f32 run;
+    * separate calls (f32 storage between predict and correct, PVFilter's own call pattern):
+      first 6 steps within 1e-4 / 1e-3, and >= 4x closer than the reference's f32 run.
     """
     g = golden("pvfilter.npz")
     dt = float(g["dt"])
@@ -119,24 +119,32 @@ def test_pvfilter_sequence_vs_reference_golden(L, golden, seed):
     err = {"x": 0.0, "P": 0.0, "x32": 0.0, "P32": 0.0}
     for step in range(g[f"s{seed}_acc"].shape[0]):
         acc, qw = t(g[f"s{seed}_acc"][step]), t(g[f"s{seed}_q_wxyz"][step])
-        L.check(L.lib.ouz_pv_predict(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, n, stream()))
         tp = t(g[f"s{seed}_trig_p"][step], torch.uint8)
         tv = t(g[f"s{seed}_trig_v"][step], torch.uint8)
         zp, zv = t(g[f"s{seed}_pos"][step]), t(g[f"s{seed}_vel"][step])
-        L.check(L.lib.ouz_pv_correct(x.data_ptr(), P.data_ptr(), zp.data_ptr(), 0, Q.PV_POS_VAR, tp.data_ptr(), n,
-                                     stream()))
-        L.check(L.lib.ouz_pv_correct(x.data_ptr(), P.data_ptr(), zv.data_ptr(), 1, 0.0, tv.data_ptr(), n, stream()))
+        if separate:   # PVFilter.prediction_step / correction_step one call each (f32 between calls)
+            L.check(L.lib.ouz_pv_predict(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, n, stream()))
+            L.check(L.lib.ouz_pv_correct(x.data_ptr(), P.data_ptr(), zp.data_ptr(), 0, Q.PV_POS_VAR, tp.data_ptr(), n,
+                                         stream()))
+            L.check(L.lib.ouz_pv_correct(x.data_ptr(), P.data_ptr(), zv.data_ptr(), 1, 0.0, tv.data_ptr(), n,
+                                         stream()))
+        else:          # the fused step's pv_step: predict + fixes in f64, f32 storage
+            L.check(L.lib.ouz_pv_step(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, zp.data_ptr(),
+                                      tp.data_ptr(), zv.data_ptr(), tv.data_ptr(), n, stream()))
         gx, gP = g[f"s{seed}_x"][step], g[f"s{seed}_P"][step]
         hx = x.cpu().numpy().astype(np.float64)
         hP = unpack_sym(P.cpu().numpy().astype(np.float64), 9)
         ex, eP = _relerr(hx, gx), _relerr(hP, gP)
-        if step < 6:
-            assert ex <= 1e-4 and eP <= 1e-4, (step, ex, eP)
+        if not separate:
+            assert ex <= 1e-3 and eP <= 1e-3, (step, ex, eP)
+        elif step < 6:
+            assert ex <= 1e-4 and eP <= 1e-3, (step, ex, eP)
         err["x"], err["P"] = max(err["x"], ex), max(err["P"], eP)
         err["x32"] = max(err["x32"], _relerr(g[f"s{seed}_x_f32ref"][step].astype(np.float64), gx))
         err["P32"] = max(err["P32"], _relerr(g[f"s{seed}_P_f32ref"][step].astype(np.float64), gP))
-    assert err["x"] * 4 <= err["x32"], err
-    assert err["P"] * 4 <= err["P32"], err
+    ratio = 4 if separate else 100
+    assert err["x"] * ratio <= err["x32"], err
+    assert err["P"] * ratio <= err["P32"], err
 
 
 def test_integrate_vs_oracle(L):
