@@ -15,7 +15,10 @@ DEPS = [SRC, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc
 OUT = os.path.join(HERE, "libouzelum_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OUZ_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
+         # f32 divide / sqrt to ~1-2 ulp instead of correctly rounded: -14 % VALU in the step kernel,
+         # well inside the parity tolerances.  f64 (PV filter) and the RNG (__f*_rn) are unaffected.
+         "-fno-hip-fp32-correctly-rounded-divide-sqrt"]
 
 
 def up_to_date() -> bool:
