@@ -181,9 +181,11 @@ OUZ_HD LeeGains default_gains() {  // controllers/control_config.py:14-17
 constexpr float kTwoPiF = 6.28318530717958647692f;
 constexpr float kPiF = 3.14159265358979323846f;
 
-// torch.remainder for floats: fmod, then shift into the divisor's sign.
+// torch.remainder for floats: fmod, then shift into the divisor's sign.  fmod(a, b) == a
+// exactly when |a| < b, which is the common case here (a = yaw command - yaw); only larger
+// arguments pay for the libm fmodf.
 OUZ_HD float remainder_f(float a, float b) {
-  float m = fmodf(a, b);
+  float m = (fabsf(a) < b) ? a : fmodf(a, b);
   if (m != 0.0f && ((b < 0.0f) != (m < 0.0f))) m += b;
   return m;
 }
