@@ -65,8 +65,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
-    ap.add_argument("--sweep", default="1048576,4194304")
+    ap.add_argument("--sweep", default="4194304,16777216")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused-rollout measurement")
     return ap.parse_args()
 
 
@@ -195,9 +196,11 @@ def main():
     rollouts(args.warmup)
     el = timed(args.steps)
     value = n * world * args.steps / el
-    rollouts(args.warmup, fused=True)
-    el_fused = timed(args.steps, fused=True)
-    value_fused = n * world * args.steps / el_fused
+    value_fused = el_fused = None
+    if not args.no_fused:
+        rollouts(args.warmup, fused=True)
+        el_fused = timed(args.steps, fused=True)
+        value_fused = n * world * args.steps / el_fused
 
     # secondary: the same steps through the Python VecTask.step() API (one ctypes call each)
     py_rate = None
@@ -227,12 +230,13 @@ def main():
                    "parallelism": f"env-sharded dp{world} (RCCL return all-reduce per 16-step rollout)"},
         "roofline": roofline_entry(args.task, n, us),
         "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
-        "fused_rollout": {"value": round(value_fused, 1), "unit": "env-steps/s",
-                          "ms_per_step": round(el_fused / args.steps * 1e3, 5),
-                          "kernel_us_per_step": round(kernel_time_us(env, ring, 320, fused=True), 3),
-                          "note": "ouz_rollout: 16 steps per launch into (16, N, ...) rollout storage, env state in "
-                                  "registers; same steps, same per-step outputs"},
     }
+    if value_fused is not None:
+        out["fused_rollout"] = {"value": round(value_fused, 1), "unit": "env-steps/s",
+                                "ms_per_step": round(el_fused / args.steps * 1e3, 5),
+                                "kernel_us_per_step": round(kernel_time_us(env, ring, 320, fused=True), 3),
+                                "note": "ouz_rollout: 16 steps per launch into (16, N, ...) rollout storage, env "
+                                        "state in registers; same steps, same per-step outputs"}
     if world == 1 and not args.no_sweep:
         sweep = []
         del env

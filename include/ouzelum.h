@@ -79,7 +79,20 @@ extern "C" {
 #define OUZ_NUM_OBS 13
 #define OUZ_NUM_ACT 4
 
-/* Per-env SoA float rows of the state buffer fstate[OUZ_F_COUNT][num_envs]. */
+/* State layout: wave-tiled SoA.  Envs are grouped in tiles of OUZ_TILE (= one
+ * wave64); a tile holds every field of its 64 envs as contiguous 64-wide rows:
+ *   fstate[ceil(num_envs/64)][OUZ_F_COUNT][64],  istate[...][OUZ_I_COUNT][64].
+ * Field f of env i lives at OUZ_FIDX(f, i, OUZ_F_COUNT).  A wave's whole state
+ * is one contiguous block, so its field loads walk DRAM pages in order instead
+ * of touching OUZ_F_COUNT rows num_envs*4 bytes apart.  Buffers must hold
+ * OUZ_TILED_SIZE(num_envs, count) elements; padding lanes are never touched. */
+#define OUZ_TILE 64
+#define OUZ_TILES(n) (((n) + OUZ_TILE - 1) / OUZ_TILE)
+#define OUZ_TILED_SIZE(n, count) ((size_t)OUZ_TILES(n) * (count) * OUZ_TILE)
+#define OUZ_FIDX(f, i, count) \
+  (((size_t)((i) / OUZ_TILE) * (count) + (f)) * OUZ_TILE + (size_t)((i) % OUZ_TILE))
+
+/* Float fields of fstate. */
 enum {
   OUZ_F_P = 0,          /* position (3)                    root_states[:, 0:3]  */
   OUZ_F_Q = 3,          /* orientation xyzw (4)            root_states[:, 3:7]  */
@@ -101,7 +114,7 @@ enum {
   OUZ_F_EP_SUM = 102,   /* sum of returns of episodes finished since last drain  */
   OUZ_F_COUNT = 103
 };
-/* Per-env SoA int32 rows of istate[OUZ_I_COUNT][num_envs]. */
+/* Int32 fields of istate. */
 enum {
   OUZ_I_PROGRESS = 0,   /* progress_buf                                         */
   OUZ_I_TRAJ_TYPE = 1,  /* 0 lemniscate, 1 circle, 2 square                     */
@@ -136,8 +149,8 @@ typedef struct ouz_config {
 } ouz_config;
 
 typedef struct ouz_buffers {
-  float* fstate;            /* [OUZ_F_COUNT][num_envs] f32                       */
-  int32_t* istate;          /* [OUZ_I_COUNT][num_envs] i32                       */
+  float* fstate;            /* [tiles][OUZ_F_COUNT][64] f32 (see OUZ_FIDX)        */
+  int32_t* istate;          /* [tiles][OUZ_I_COUNT][64] i32                       */
   float* obs;               /* [num_envs][13] f32, clamped to +-5 (vec_task.py:353) */
   float* rew;               /* [num_envs] f32                                    */
   int64_t* reset;           /* [num_envs] i64  reset_buf                         */

@@ -36,6 +36,11 @@ F_EP_RET, F_EP_SUM = 101, 102
 F_COUNT = 103
 I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT = range(8)
 I_COUNT = 8
+TILE = 64  # OUZ_TILE: state is [tiles][fields][64] (ouzelum.h OUZ_FIDX)
+
+
+def tiles(n):
+    return (n + TILE - 1) // TILE
 
 
 class OuzConfig(ctypes.Structure):

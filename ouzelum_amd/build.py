@@ -31,7 +31,8 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
-    cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", SRC]
+    extra = os.environ.get("OUZ_EXTRA_FLAGS", "").split()
+    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

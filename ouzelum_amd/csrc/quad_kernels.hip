@@ -1,9 +1,9 @@
 // Fused per-env quadrotor step for MI355X (gfx950) + the C ABI of include/ouzelum.h.
 //
 // Design:
-//  * one env per lane, wave64; per-env state is SoA f32 rows in HBM
-//    (fstate[field][env]) so every field load/store of a wave is one
-//    coalesced 256-byte transaction;
+//  * one env per lane, wave64; per-env state is wave-tiled SoA f32 in HBM
+//    (fstate[tile][field][64]) so every field load/store of a wave is one
+//    coalesced 256-byte transaction and a wave's whole state is contiguous;
 //  * the whole VecTask.step — lazy reset, controller / estimator, wrench,
 //    2 integration sub-steps, reward/done/obs — is ONE kernel launch with no
 //    host synchronisation (the reference does reset_buf.nonzero() + per-env
@@ -139,10 +139,15 @@ __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int 
   }
 }
 
-__device__ __forceinline__ float ld(const StepArgs& a, int field, int i) { return a.f[(size_t)field * a.n + i]; }
-__device__ __forceinline__ void st(const StepArgs& a, int field, int i, float v) { a.f[(size_t)field * a.n + i] = v; }
-__device__ __forceinline__ int32_t ldi(const StepArgs& a, int field, int i) { return a.iv[(size_t)field * a.n + i]; }
-__device__ __forceinline__ void sti(const StepArgs& a, int field, int i, int32_t v) { a.iv[(size_t)field * a.n + i] = v; }
+// Wave-tiled SoA (include/ouzelum.h OUZ_FIDX): a wave's fields are contiguous
+// 256-byte rows, field f at offset f*256 from the wave's tile base.
+__device__ __forceinline__ size_t fidx(int field, int i, int count) {
+  return ((size_t)(i >> 6) * count + field) * 64 + (i & 63);
+}
+__device__ __forceinline__ float ld(const StepArgs& a, int field, int i) { return a.f[fidx(field, i, OUZ_F_COUNT)]; }
+__device__ __forceinline__ void st(const StepArgs& a, int field, int i, float v) { a.f[fidx(field, i, OUZ_F_COUNT)] = v; }
+__device__ __forceinline__ int32_t ldi(const StepArgs& a, int field, int i) { return a.iv[fidx(field, i, OUZ_I_COUNT)]; }
+__device__ __forceinline__ void sti(const StepArgs& a, int field, int i, int32_t v) { a.iv[fidx(field, i, OUZ_I_COUNT)] = v; }
 __device__ __forceinline__ V3 ld3(const StepArgs& a, int f, int i) { return v3(ld(a, f, i), ld(a, f + 1, i), ld(a, f + 2, i)); }
 __device__ __forceinline__ void st3(const StepArgs& a, int f, int i, V3 v) { st(a, f, i, v.x); st(a, f + 1, i, v.y); st(a, f + 2, i, v.z); }
 
@@ -511,9 +516,19 @@ struct OutPtrs {
 };
 
 __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, int n, bool valid, const float* ob,
-                                     float rew, bool rs, bool to) {
+                                     float rew, bool rs, bool to, bool direct) {
   const int lane = threadIdx.x & 63;
   const int first = i - lane;
+  if (direct) {   // wave shared by two tasks (misaligned mixed shard): plain per-lane stores
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < OUZ_NUM_OBS; ++k) o.obs[(size_t)i * OUZ_NUM_OBS + k] = ob[k];
+      o.rew[i] = rew;
+      o.reset[i] = rs ? 1 : 0;
+      o.timeouts[i] = to ? 1 : 0;
+    }
+    return;
+  }
   if (valid) {
 #pragma unroll
     for (int k = 0; k < OUZ_NUM_OBS; ++k) wave_lds[lane * OUZ_NUM_OBS + k] = ob[k];
@@ -535,7 +550,8 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
 // VecTask.step kernel (K = 1, no loop, no rollout storage) and keeps the register budget of one step.
 template <int CTRL, int TGT, bool MULTI>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
-                                        size_t out_stride, float* wave_lds, int i, bool valid, int task) {
+                                        size_t out_stride, float* wave_lds, int i, bool valid, int task,
+                                        bool direct = false) {
   const TaskParams& tp = a.tp[task];
   const uint32_t gid = a.env_offset + (uint32_t)i;
   EnvRegs<CTRL, TGT> S;
@@ -545,7 +561,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     float rew = 0.0f;
     bool rs = false, to = false;
     if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
-    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to);
+    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
   } else {
     for (int k = 0; k < K; ++k) {
       float ob[OUZ_NUM_OBS];
@@ -558,10 +574,10 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
         o.rew += (size_t)k * out_stride;
         o.reset += (size_t)k * out_stride;
         o.timeouts += (size_t)k * out_stride;
-        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to);
-        if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to);
+        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+        if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
       } else {
-        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to);
+        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
       }
     }
   }
@@ -594,13 +610,22 @@ __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, Rollou
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
     run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
   } else {
-    const int t = mixed_task(a.env_offset + (uint32_t)first);   // wave-uniform: 64-env blocks
-    if (t == OUZ_TASK_LEE_LANDED)
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
-    else if (t == OUZ_TASK_TRACKING)
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
-    else
-      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, t);
+    // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
+    // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
+    // alignments execute the same code, so a sharded run stays bit-identical to the unsharded one.
+    const int t = mixed_task(a.env_offset + (uint32_t)i);
+    const bool direct = (a.env_offset & 63) != 0;   // a wave straddles two blocks: no LDS obs staging
+    const bool vl = valid && t == OUZ_TASK_LEE_LANDED, vt = valid && t == OUZ_TASK_TRACKING;
+    const bool vr = valid && !vl && !vt;
+    if (__any(vl))
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vl,
+                                                  OUZ_TASK_LEE_LANDED, direct);
+    if (__any(vt))
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vt,
+                                             OUZ_TASK_TRACKING, direct);
+    if (__any(vr))
+      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
+                                        direct);
   }
 }
 
@@ -878,7 +903,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   r = hip_check(hipMalloc(&e->wp_tab, sizeof(host_tab)), "hipMalloc(waypoints)");
   if (r) { delete e; return r; }
   r = hip_check(hipMemcpy(e->wp_tab, host_tab, sizeof(host_tab), hipMemcpyHostToDevice), "hipMemcpy(waypoints)");
-  if (r) { hipFree(e->wp_tab); delete e; return r; }
+  if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
   StepArgs& a = e->args;
   std::memset(&a, 0, sizeof(a));
   a.wp_tab = e->wp_tab;
@@ -917,7 +942,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
 
 int ouz_destroy(ouz_env* env) {
   if (!env) return OUZ_OK;
-  if (env->wp_tab) hipFree(env->wp_tab);
+  if (env->wp_tab) (void)hipFree(env->wp_tab);
   delete env;
   return OUZ_OK;
 }

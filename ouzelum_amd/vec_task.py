@@ -102,8 +102,9 @@ class QuadVecTask:
 
         # --- buffers (owned here; allocate_buffers vec_task.py:254-277) ---
         with torch.cuda.device(self.device):
-            self.fstate = torch.empty((L.F_COUNT, n), dtype=torch.float32, device=self.device)
-            self.istate = torch.empty((L.I_COUNT, n), dtype=torch.int32, device=self.device)
+            # wave-tiled SoA [tiles][fields][64] (include/ouzelum.h OUZ_FIDX); padding lanes stay 0
+            self.fstate = torch.zeros((L.tiles(n), L.F_COUNT, L.TILE), dtype=torch.float32, device=self.device)
+            self.istate = torch.zeros((L.tiles(n), L.I_COUNT, L.TILE), dtype=torch.int32, device=self.device)
             self.obs_buf = torch.empty((n, L.NUM_OBS), dtype=torch.float32, device=self.device)
             self.rew_buf = torch.empty(n, dtype=torch.float32, device=self.device)
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -156,15 +157,27 @@ class QuadVecTask:
     def num_obs(self) -> int:
         return self.num_observations
 
+    def frows(self, f0, f1=None):
+        """Float fields [f0, f1) as a (k, N) tensor (a copy: the tiled layout has no flat row view)."""
+        f1 = f0 + 1 if f1 is None else f1
+        t = self.fstate[:, f0:f1, :].permute(1, 0, 2).reshape(f1 - f0, -1)
+        return t[:, :self.num_envs]
+
+    def irows(self, f0, f1=None):
+        """Int32 fields [f0, f1) as a (k, N) tensor (copy)."""
+        f1 = f0 + 1 if f1 is None else f1
+        t = self.istate[:, f0:f1, :].permute(1, 0, 2).reshape(f1 - f0, -1)
+        return t[:, :self.num_envs]
+
     @property
     def progress_buf(self):
-        """progress_buf (int32 SoA row; the reference keeps int64)."""
-        return self.istate[L.I_PROGRESS]
+        """progress_buf (int32; the reference keeps int64).  A snapshot copy."""
+        return self.irows(L.I_PROGRESS)[0]
 
     @property
     def root_states(self):
-        """(N, 13) view [p, q_xyzw, v, w] of the SoA state (ekf_lee_landed.py:84)."""
-        return self.fstate[0:13].t()
+        """(N, 13) [p, q_xyzw, v, w] (ekf_lee_landed.py:84).  A snapshot copy of the tiled state."""
+        return self.frows(0, 13).t()
 
     def env_task_ids(self):
         """Per-env task id (the mixed curriculum assigns tasks per 64-env block of global ids)."""
@@ -178,7 +191,7 @@ class QuadVecTask:
     def target_root_positions(self):
         """(N, 3) target_root_positions.  Random goals are stored state; a landing-platform target
         is platform xy + offset at z 0.377 and is recomputed here (the kernel never stores it)."""
-        tgt = self.fstate[L.F_TARGET:L.F_TARGET + 3].t().clone()
+        tgt = self.frows(L.F_TARGET, L.F_TARGET + 3).t().clone()
         tids = self.env_task_ids()
         started = self.sim_step_count > 0
         for t in tids.unique().tolist():
@@ -186,7 +199,7 @@ class QuadVecTask:
             if info.target_mode == L.TGT_GOAL:
                 continue
             m = tids == t
-            plat = self.fstate[L.F_PLAT:L.F_PLAT + 2].t()[m] if info.target_mode == L.TGT_TRAJ else \
+            plat = self.frows(L.F_PLAT, L.F_PLAT + 2).t()[m] if info.target_mode == L.TGT_TRAJ else \
                 torch.zeros((int(m.sum()), 2), device=self.device)
             tgt[m, 0] = plat[:, 0] + info.plat_offset_x if started else 0.0
             tgt[m, 1] = plat[:, 1] if started else 0.0
@@ -199,7 +212,7 @@ class QuadVecTask:
 
     def landings(self) -> int:
         """Total landings over all finished episodes (ekf_lee_landed.py:319-331 'Landoa')."""
-        return int(self.istate[L.I_LANDINGS].sum().item())
+        return int(self.istate[:, L.I_LANDINGS].sum().item())
 
     def episode_stats(self, drain=True):
         """(sum of returns, count) of episodes finished since the last drain, as a float64
@@ -207,10 +220,11 @@ class QuadVecTask:
         Needs ``track_episodes=True`` (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35)."""
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
-        out = torch.stack([self.fstate[L.F_EP_SUM].double().sum(), self.istate[L.I_EP_CNT].double().sum()])
+        # padding lanes are never written, so summing whole tiles is exact
+        out = torch.stack([self.fstate[:, L.F_EP_SUM].double().sum(), self.istate[:, L.I_EP_CNT].double().sum()])
         if drain:
-            self.fstate[L.F_EP_SUM].zero_()
-            self.istate[L.I_EP_CNT].zero_()
+            self.fstate[:, L.F_EP_SUM].zero_()
+            self.istate[:, L.I_EP_CNT].zero_()
         return out
 
     def zero_actions(self):

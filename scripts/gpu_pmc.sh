@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 cd /tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $C -d "$R/gpurun_out/pmc_${TAG}_${TASK}_${N}_$C" -o run --output-format csv -- \
-    python3 "$R/bench.py" --task "$TASK" --num-envs "$N" --steps "$STEPS" --warmup 10 --no-cpu-baseline --no-sweep \
+    python3 "$R/bench.py" --task "$TASK" --num-envs "$N" --steps "$STEPS" --warmup 10 --no-cpu-baseline --no-sweep --no-fused \
     > /dev/null 2> "$R/gpurun_out/pmc_${TAG}_${TASK}_${N}_$C.err" || exit $?
 done
 python3 "$R/scripts/pmc_summarize.py" "$R/gpurun_out" "$TAG" "$TASK" "$N"

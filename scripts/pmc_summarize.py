@@ -16,7 +16,9 @@ def avg_counter(path_glob, counter):
     for f in glob.glob(path_glob, recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "quad_step_kernel" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                name = row.get("Kernel_Name", "")
+                # the single-step launch (quad_step_kernel<TASK, false>), not the fused rollout variant
+                if "quad_step_kernel" in name and "false>" in name and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 

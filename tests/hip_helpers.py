@@ -43,8 +43,8 @@ def gpu_to_oracle(env, oenv):
     """Copy a QuadVecTask's full state into an OracleEnv (float64)."""
     from ouzelum_amd import _lib as L
     torch.cuda.synchronize()
-    f = env.fstate.cpu().numpy().astype(np.float64)
-    iv = env.istate.cpu().numpy().astype(np.int64)
+    f = env.frows(0, L.F_COUNT).cpu().numpy().astype(np.float64)
+    iv = env.irows(0, L.I_COUNT).cpu().numpy().astype(np.int64)
     oenv.p = f[L.F_P:L.F_P + 3].T.copy()
     oenv.q = f[L.F_Q:L.F_Q + 4].T.copy()
     oenv.v = f[L.F_V:L.F_V + 3].T.copy()
@@ -75,8 +75,8 @@ def gpu_to_oracle(env, oenv):
 def gpu_snapshot(env):
     from ouzelum_amd import _lib as L
     torch.cuda.synchronize()
-    f = env.fstate.cpu().numpy().astype(np.float64)
-    iv = env.istate.cpu().numpy()
+    f = env.frows(0, L.F_COUNT).cpu().numpy().astype(np.float64)
+    iv = env.irows(0, L.I_COUNT).cpu().numpy()
     return {
         "p": f[0:3].T, "q": f[3:7].T, "v": f[7:10].T, "w": f[10:13].T,
         "target": env.target_root_positions.cpu().numpy().astype(np.float64), "thrust": f[L.F_THRUST:L.F_THRUST + 4].T,

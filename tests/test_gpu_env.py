@@ -145,8 +145,10 @@ def test_deterministic_rerun(ouz, task):
 @pytest.mark.parametrize("task", ["EKFLeeLanded", "QuadMixed", "QuadFault"])
 def test_shard_invariance(ouz, task):
     """Envs sharded over 2 'ranks' (env_id_offset) reproduce the unsharded run bit for bit:
-    every draw and the shared PV trigger index are keyed on the global env id."""
-    n = 512
+    every draw and the shared PV trigger index are keyed on the global env id.
+    456 = 2 x 228: both shards end in a partial 64-env tile."""
+    from ouzelum_amd import _lib as L
+    n = 456
     full = ouz.make(seed=7, task=task, num_envs=n, sim_device="cuda:0", convergence_time=10)
     halves = [ouz.make(seed=7, task=task, num_envs=n // 2, sim_device="cuda:0", env_id_offset=r * n // 2,
                        num_envs_total=n, convergence_time=10) for r in range(2)]
@@ -157,7 +159,8 @@ def test_shard_invariance(ouz, task):
         halves[0].step(a[: n // 2].contiguous())
         halves[1].step(a[n // 2:].contiguous())
     torch.cuda.synchronize()
-    assert torch.equal(full.fstate, torch.cat([h.fstate for h in halves], 1))
+    assert torch.equal(full.frows(0, L.F_COUNT), torch.cat([h.frows(0, L.F_COUNT) for h in halves], 1))
+    assert torch.equal(full.irows(0, L.I_COUNT), torch.cat([h.irows(0, L.I_COUNT) for h in halves], 1))
     assert torch.equal(full.obs_buf, torch.cat([h.obs_buf for h in halves], 0))
     assert torch.equal(full.reset_buf, torch.cat([h.reset_buf for h in halves], 0))
 
@@ -207,10 +210,10 @@ def test_baseline_size_properties(ouz, task, n):
     for _ in range(30):
         env.step(torch.rand((n, 4), device="cuda", generator=g) * 2 - 1)
     torch.cuda.synchronize()
-    assert bool(torch.isfinite(env.fstate[0:13]).all())
+    assert bool(torch.isfinite(env.frows(0, 13)).all())
     assert bool(torch.isfinite(env.rew_buf).all()) and float(env.obs_buf.abs().max()) <= 5.0
     assert bool((env.timeout_buf.long() <= env.reset_buf).all())
-    qn = env.fstate[3:7].norm(dim=0)
+    qn = env.frows(3, 7).norm(dim=0)
     assert float((qn - 1).abs().max()) < 1e-5
 
 
