@@ -185,6 +185,13 @@ int ouz_rollout(ouz_env* env, const float* action_ring, int32_t ring_len, int32_
                 float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, void* stream);
 int ouz_reset_idx(ouz_env* env, const int32_t* env_ids, int32_t n, void* stream);
 int ouz_reset_all(ouz_env* env, void* stream);
+/* Episode statistics of envs created with track_episodes: writes the f64 pair
+ * out[0] = sum of returns, out[1] = count, of the episodes finished since the
+ * last drain (device pointer, stream-ordered; one launch, deterministic order).
+ * drain != 0 zeroes the accumulators.  Replaces RecordEpisodeStatisticsTorch's
+ * per-step host bookkeeping (PPO/utils.py:20-35); the pair is what config E
+ * all-reduces over RCCL. */
+int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream);
 int64_t ouz_get_step(const ouz_env* env);
 int ouz_set_step(ouz_env* env, int64_t step);
 

@@ -87,6 +87,7 @@ SIGNATURES = {
     "ouz_rollout": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
     "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
     "ouz_reset_all": (_I, [_P, _P]),
+    "ouz_episode_stats": (_I, [_P, _P, _I, _P]),
     "ouz_get_step": (_I64, [_P]),
     "ouz_set_step": (_I, [_P, _I64]),
     "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),

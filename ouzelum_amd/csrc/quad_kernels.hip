@@ -669,6 +669,59 @@ __global__ void mark_all_kernel(int64_t* reset, int32_t n) {
   if (k < n) reset[k] = 1;
 }
 
+// Episode statistics in one launch (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35): [sum of
+// finished-episode returns, count] over all envs, optionally drained.  Each block reduces a fixed
+// grid-stride slice into partials[block]; the last block to finish (ticket counter) adds the
+// partials in block order, so the result is deterministic run to run.
+constexpr int kStatsBlock = 256;
+constexpr int kStatsMaxBlocks = 256;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, double2* partials, uint32_t* ticket,
+                                                                    double* out, int drain) {
+  __shared__ double s_sum[kStatsBlock / 64], s_cnt[kStatsBlock / 64];
+  __shared__ bool s_last;
+  double sum = 0.0, cnt = 0.0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+    sum += (double)ld(a, OUZ_F_EP_SUM, i);
+    cnt += (double)ldi(a, OUZ_I_EP_CNT, i);
+    if (drain) {
+      st(a, OUZ_F_EP_SUM, i, 0.0f);
+      sti(a, OUZ_I_EP_CNT, i, 0);
+    }
+  }
+  sum = wave_sum(sum);
+  cnt = wave_sum(cnt);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { s_sum[w] = sum; s_cnt[w] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double2 p{0.0, 0.0};
+    for (int k = 0; k < kStatsBlock / 64; ++k) { p.x += s_sum[k]; p.y += s_cnt[k]; }
+    partials[blockIdx.x] = p;
+    __threadfence();
+    s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    __threadfence();
+    double2 t{0.0, 0.0};
+    for (unsigned b = 0; b < gridDim.x; ++b) {
+      const double2 p = partials[b];
+      t.x += p.x;
+      t.y += p.y;
+    }
+    out[0] = t.x;
+    out[1] = t.y;
+    *ticket = 0u;   // ready for the next launch on this stream
+  }
+}
+
 // ---------------------------------------------------------------------------
 // component kernels (AoS in/out; parity entry points)
 // ---------------------------------------------------------------------------
@@ -827,6 +880,8 @@ struct ouz_env {
   bool bound;
   int64_t step;
   float2* wp_tab;   // device waypoint tables
+  double2* stats_partials;   // [kStatsMaxBlocks] per-block partials of episode_stats_kernel
+  uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
 };
 
@@ -904,6 +959,12 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   if (r) { delete e; return r; }
   r = hip_check(hipMemcpy(e->wp_tab, host_tab, sizeof(host_tab), hipMemcpyHostToDevice), "hipMemcpy(waypoints)");
   if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
+  r = hip_check(hipMalloc(&e->stats_partials, kStatsMaxBlocks * sizeof(double2) + sizeof(uint32_t)),
+                "hipMalloc(stats)");
+  if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
+  e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks);
+  r = hip_check(hipMemset(e->stats_ticket, 0, sizeof(uint32_t)), "hipMemset(stats)");
+  if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   StepArgs& a = e->args;
   std::memset(&a, 0, sizeof(a));
   a.wp_tab = e->wp_tab;
@@ -943,6 +1004,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
 int ouz_destroy(ouz_env* env) {
   if (!env) return OUZ_OK;
   if (env->wp_tab) (void)hipFree(env->wp_tab);
+  if (env->stats_partials) (void)hipFree(env->stats_partials);
   delete env;
   return OUZ_OK;
 }
@@ -1094,6 +1156,19 @@ int ouz_reset_all(ouz_env* env, void* stream) {
   const int n = env->cfg.num_envs;
   hipLaunchKernelGGL(mark_all_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, env->buf.reset, n);
   OUZ_LAUNCH_CHECK("mark_all_kernel");
+  return OUZ_OK;
+}
+
+int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream) {
+  if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_episode_stats: env not bound");
+  if (!out) return fail(OUZ_ERR_INVALID, "ouz_episode_stats: null out");
+  if (!env->cfg.track_episodes) return fail(OUZ_ERR_INVALID, "ouz_episode_stats: env created without track_episodes");
+  const int n = env->cfg.num_envs;
+  int grid = grid_for(n, kStatsBlock);
+  if (grid > kStatsMaxBlocks) grid = kStatsMaxBlocks;
+  hipLaunchKernelGGL(episode_stats_kernel, dim3(grid), dim3(kStatsBlock), 0, (hipStream_t)stream, env->args,
+                     env->stats_partials, env->stats_ticket, out, drain ? 1 : 0);
+  OUZ_LAUNCH_CHECK("episode_stats_kernel");
   return OUZ_OK;
 }
 

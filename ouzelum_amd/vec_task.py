@@ -110,6 +110,7 @@ class QuadVecTask:
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
             self.timeout_buf = torch.empty(n, dtype=torch.bool, device=self.device)
             self._zero_actions = torch.zeros((n, L.NUM_ACT), dtype=torch.float32, device=self.device)
+            self._stats_buf = torch.zeros(2, dtype=torch.float64, device=self.device)
         self.states_buf = torch.zeros((n, 0), dtype=torch.float32, device=self.device)
         self.extras = {}
         self.obs_dict = {}
@@ -216,16 +217,15 @@ class QuadVecTask:
 
     def episode_stats(self, drain=True):
         """(sum of returns, count) of episodes finished since the last drain, as a float64
-        device tensor [sum, count] — the quantity config E all-reduces over RCCL.
+        device tensor [sum, count] — the quantity config E all-reduces over RCCL.  One kernel
+        (``ouz_episode_stats``).  The tensor is returned by reference and overwritten by the next
+        call, like ``rew_buf``; clone it to keep it.
         Needs ``track_episodes=True`` (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35)."""
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
-        # padding lanes are never written, so summing whole tiles is exact
-        out = torch.stack([self.fstate[:, L.F_EP_SUM].double().sum(), self.istate[:, L.I_EP_CNT].double().sum()])
-        if drain:
-            self.fstate[:, L.F_EP_SUM].zero_()
-            self.istate[:, L.I_EP_CNT].zero_()
-        return out
+        L.check(L.lib.ouz_episode_stats(self._env, L.ptr(self._stats_buf), 1 if drain else 0, self._stream()),
+                "ouz_episode_stats")
+        return self._stats_buf
 
     def zero_actions(self):
         return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)

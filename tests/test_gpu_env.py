@@ -246,3 +246,31 @@ def test_fused_rollout_matches_single_steps(ouz, task):
     assert torch.equal(a.istate, b.istate)
     assert torch.equal(a.reset_buf, b.reset_buf) and torch.equal(a.obs_buf, obs_s[-1])
     assert a.sim_step_count == b.sim_step_count == K
+
+
+@pytest.mark.parametrize("task,n", [("Ouzelum", 1000), ("QuadFault", 70000), ("QuadMixed", 4096)])
+def test_episode_stats_kernel(ouz, task, n):
+    """ouz_episode_stats (one launch) == RecordEpisodeStatisticsTorch bookkeeping done on the
+    step outputs (PPO/utils.py:20-35): returns accumulate per env, a done adds the episode's
+    return to the sum and bumps the count.  70000 envs > 256 blocks x 256 exercises the grid stride."""
+    env = ouz.make(seed=4, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ep_ret = torch.zeros(n, dtype=torch.float64, device="cuda")
+    tot = torch.zeros(2, dtype=torch.float64, device="cuda")
+    for k in range(60):
+        env.step(torch.rand((n, 4), device="cuda", generator=g) * 2 - 1)
+        ep_ret += env.rew_buf.double()
+        done = env.reset_buf.bool()
+        tot[0] += ep_ret[done].sum()
+        tot[1] += done.sum()
+        ep_ret[done] = 0
+        if k == 29:   # a non-draining peek, then a drain half way
+            peek = env.episode_stats(drain=False).clone()
+            mid = env.episode_stats().clone()
+            assert torch.equal(peek, mid)
+            torch.testing.assert_close(mid, tot, rtol=1e-5, atol=1e-3)
+            tot.zero_()
+    end = env.episode_stats().clone()
+    assert float(tot[1]) > 0, "no episode finished: the test would not test anything"
+    torch.testing.assert_close(end, tot, rtol=1e-5, atol=1e-3)
+    assert float(env.episode_stats()[1]) == 0.0          # drained
