@@ -137,7 +137,15 @@ def ptr(t) -> int | None:
     return t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(device=None) -> int:
+    """hipStream_t of torch's current stream on ``device``.  The raw accessor costs ~0.1 us
+    against ~2 us for ``torch.cuda.current_stream().cuda_stream`` — a third of a step call."""
+    if _raw_stream is not None:
+        idx = device.index if isinstance(device, torch.device) else device
+        return _raw_stream(torch.cuda.current_device() if idx is None else idx)
     return torch.cuda.current_stream(device).cuda_stream
 
 

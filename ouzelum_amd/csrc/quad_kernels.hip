@@ -140,16 +140,42 @@ __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int 
 }
 
 // Wave-tiled SoA (include/ouzelum.h OUZ_FIDX): a wave's fields are contiguous
-// 256-byte rows, field f at offset f*256 from the wave's tile base.
-__device__ __forceinline__ size_t fidx(int field, int i, int count) {
-  return ((size_t)(i >> 6) * count + field) * 64 + (i & 63);
+// 256-byte rows, field f at offset f*256 from the wave's tile base.  The tile base is
+// wave-uniform (readfirstlane -> SGPR pair), the per-lane part a 32-bit offset, so every
+// access is one `global_load/store v, v_off, s[base] offset:f*256` with no 64-bit VALU
+// address arithmetic and no VGPR pairs held for pointers.
+__device__ __forceinline__ uint32_t wave_tile(int i) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)i >> 6);
 }
-__device__ __forceinline__ float ld(const StepArgs& a, int field, int i) { return a.f[fidx(field, i, OUZ_F_COUNT)]; }
-__device__ __forceinline__ void st(const StepArgs& a, int field, int i, float v) { a.f[fidx(field, i, OUZ_F_COUNT)] = v; }
-__device__ __forceinline__ int32_t ldi(const StepArgs& a, int field, int i) { return a.iv[fidx(field, i, OUZ_I_COUNT)]; }
-__device__ __forceinline__ void sti(const StepArgs& a, int field, int i, int32_t v) { a.iv[fidx(field, i, OUZ_I_COUNT)] = v; }
+__device__ __forceinline__ float* ftile(const StepArgs& a, int i) {
+  return a.f + (size_t)wave_tile(i) * (OUZ_F_COUNT * 64);
+}
+__device__ __forceinline__ int32_t* itile(const StepArgs& a, int i) {
+  return a.iv + (size_t)wave_tile(i) * (OUZ_I_COUNT * 64);
+}
+__device__ __forceinline__ uint32_t lane_off(int field, int i) { return (uint32_t)field * 64u + ((uint32_t)i & 63u); }
+__device__ __forceinline__ float ld(const StepArgs& a, int field, int i) { return ftile(a, i)[lane_off(field, i)]; }
+__device__ __forceinline__ void st(const StepArgs& a, int field, int i, float v) { ftile(a, i)[lane_off(field, i)] = v; }
+__device__ __forceinline__ int32_t ldi(const StepArgs& a, int field, int i) { return itile(a, i)[lane_off(field, i)]; }
+__device__ __forceinline__ void sti(const StepArgs& a, int field, int i, int32_t v) { itile(a, i)[lane_off(field, i)] = v; }
 __device__ __forceinline__ V3 ld3(const StepArgs& a, int f, int i) { return v3(ld(a, f, i), ld(a, f + 1, i), ld(a, f + 2, i)); }
 __device__ __forceinline__ void st3(const StepArgs& a, int f, int i, V3 v) { st(a, f, i, v.x); st(a, f + 1, i, v.y); st(a, f + 2, i, v.z); }
+// One wave's tile, resolved once per env pass: uniform base pointers + this lane's index.
+struct Tile {
+  float* f;
+  int32_t* iv;
+  uint32_t l;       // lane = env index within the tile
+  uint32_t first;   // env index of lane 0 (wave-uniform)
+};
+__device__ __forceinline__ Tile tile_of(const StepArgs& a, int i) {
+  return Tile{ftile(a, i), itile(a, i), (uint32_t)i & 63u, wave_tile(i) * 64u};
+}
+__device__ __forceinline__ float ld(const Tile& t, int field) { return t.f[(uint32_t)field * 64u + t.l]; }
+__device__ __forceinline__ void st(const Tile& t, int field, float v) { t.f[(uint32_t)field * 64u + t.l] = v; }
+__device__ __forceinline__ int32_t ldi(const Tile& t, int field) { return t.iv[(uint32_t)field * 64u + t.l]; }
+__device__ __forceinline__ void sti(const Tile& t, int field, int32_t v) { t.iv[(uint32_t)field * 64u + t.l] = v; }
+__device__ __forceinline__ V3 ld3(const Tile& t, int f) { return v3(ld(t, f), ld(t, f + 1), ld(t, f + 2)); }
+__device__ __forceinline__ void st3(const Tile& t, int f, V3 v) { st(t, f, v.x); st(t, f + 1, v.y); st(t, f + 2, v.z); }
 
 __device__ __forceinline__ float2 traj_point(const StepArgs& a, int type, int idx, float sd) {
   int len = type == 0 ? kTrajLen[0] : (type == 1 ? kTrajLen[1] : kTrajLen[2]);
@@ -168,6 +194,7 @@ enum Dirty : uint32_t { D_DR = 1, D_FAULT = 2, D_TRAJ = 4, D_LAND = 8 };
 
 template <int CTRL, int TGT>
 struct EnvRegs {
+  Tile T;                         // this env's tile in fstate / istate
   V3 p, v, w;
   Q4 q;
   int32_t progress;
@@ -191,43 +218,43 @@ struct EnvRegs {
 
 template <int CTRL, int TGT>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S) {
-  S.rst = a.reset[i] != 0;
-  S.p = ld3(a, OUZ_F_P, i);
-  S.q = Q4{ld(a, OUZ_F_Q, i), ld(a, OUZ_F_Q + 1, i), ld(a, OUZ_F_Q + 2, i), ld(a, OUZ_F_Q + 3, i)};
-  S.v = ld3(a, OUZ_F_V, i);
-  S.w = ld3(a, OUZ_F_W, i);
-  S.progress = ldi(a, OUZ_I_PROGRESS, i);
+  S.rst = (a.reset + S.T.first)[S.T.l] != 0;
+  S.p = ld3(S.T, OUZ_F_P);
+  S.q = Q4{ld(S.T, OUZ_F_Q), ld(S.T, OUZ_F_Q + 1), ld(S.T, OUZ_F_Q + 2), ld(S.T, OUZ_F_Q + 3)};
+  S.v = ld3(S.T, OUZ_F_V);
+  S.w = ld3(S.T, OUZ_F_W);
+  S.progress = ldi(S.T, OUZ_I_PROGRESS);
   S.dirty = 0;
   S.land_flag = -1;
   S.landings_add = 0;
   S.ep_cnt_add = 0;
   S.ep_sum_add = 0.0f;
-  S.ep_ret = a.track_episodes ? ld(a, OUZ_F_EP_RET, i) : 0.0f;
+  S.ep_ret = a.track_episodes ? ld(S.T, OUZ_F_EP_RET) : 0.0f;
   S.dr_m = S.dr_i = S.dr_t = 1.0f;
-  if (tp.dr) { S.dr_m = ld(a, OUZ_F_DR, i); S.dr_i = ld(a, OUZ_F_DR + 1, i); S.dr_t = ld(a, OUZ_F_DR + 2, i); }
-  if constexpr (TGT == TGT_GOAL) S.target = ld3(a, OUZ_F_TARGET, i);
+  if (tp.dr) { S.dr_m = ld(S.T, OUZ_F_DR); S.dr_i = ld(S.T, OUZ_F_DR + 1); S.dr_t = ld(S.T, OUZ_F_DR + 2); }
+  if constexpr (TGT == TGT_GOAL) S.target = ld3(S.T, OUZ_F_TARGET);
   if constexpr (CTRL == CTRL_RL) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) S.thrust[k] = ld(a, OUZ_F_THRUST + k, i);
+    for (int k = 0; k < 4; ++k) S.thrust[k] = ld(S.T, OUZ_F_THRUST + k);
     S.frot = -1; S.fonset = 0; S.eta = 1.0f;
-    if (tp.fault) { S.frot = ldi(a, OUZ_I_FAULT_ROTOR, i); S.fonset = ldi(a, OUZ_I_FAULT_ONSET, i); S.eta = ld(a, OUZ_F_FAULT_ETA, i); }
+    if (tp.fault) { S.frot = ldi(S.T, OUZ_I_FAULT_ROTOR); S.fonset = ldi(S.T, OUZ_I_FAULT_ONSET); S.eta = ld(S.T, OUZ_F_FAULT_ETA); }
   }
   if constexpr (CTRL == CTRL_LEE_EST) {
-    S.prev_v = ld3(a, OUZ_F_PREV_V, i);
-    S.wp = ld3(a, OUZ_F_WAYPOINT, i);
-    S.eq = EkfQ{ld(a, OUZ_F_EKF_Q, i), ld(a, OUZ_F_EKF_Q + 1, i), ld(a, OUZ_F_EKF_Q + 2, i), ld(a, OUZ_F_EKF_Q + 3, i)};
+    S.prev_v = ld3(S.T, OUZ_F_PREV_V);
+    S.wp = ld3(S.T, OUZ_F_WAYPOINT);
+    S.eq = EkfQ{ld(S.T, OUZ_F_EKF_Q), ld(S.T, OUZ_F_EKF_Q + 1), ld(S.T, OUZ_F_EKF_Q + 2), ld(S.T, OUZ_F_EKF_Q + 3)};
 #pragma unroll
-    for (int k = 0; k < 10; ++k) S.eP[k] = ld(a, OUZ_F_EKF_P + k, i);
+    for (int k = 0; k < 10; ++k) S.eP[k] = ld(S.T, OUZ_F_EKF_P + k);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) S.px[k] = ld(a, OUZ_F_PV_X + k, i);
+    for (int k = 0; k < 9; ++k) S.px[k] = ld(S.T, OUZ_F_PV_X + k);
 #pragma unroll
-    for (int k = 0; k < 45; ++k) S.pP[k] = ld(a, OUZ_F_PV_P + k, i);
+    for (int k = 0; k < 45; ++k) S.pP[k] = ld(S.T, OUZ_F_PV_P + k);
   }
   if constexpr (TGT == TGT_TRAJ) {
-    S.plat = make_float2(ld(a, OUZ_F_PLAT, i), ld(a, OUZ_F_PLAT + 1, i));
-    S.ttype = ldi(a, OUZ_I_TRAJ_TYPE, i);
-    S.tidx = ldi(a, OUZ_I_TRAJ_IDX, i);
-    S.sd = ld(a, OUZ_F_TRAJ_SD, i);
+    S.plat = make_float2(ld(S.T, OUZ_F_PLAT), ld(S.T, OUZ_F_PLAT + 1));
+    S.ttype = ldi(S.T, OUZ_I_TRAJ_TYPE);
+    S.tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
+    S.sd = ld(S.T, OUZ_F_TRAJ_SD);
   } else {
     S.plat = make_float2(0.0f, 0.0f);
   }
@@ -235,42 +262,42 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
 
 template <int CTRL, int TGT>
 __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskParams& tp, const EnvRegs<CTRL, TGT>& S) {
-  st3(a, OUZ_F_P, i, S.p);
-  st(a, OUZ_F_Q, i, S.q.x); st(a, OUZ_F_Q + 1, i, S.q.y); st(a, OUZ_F_Q + 2, i, S.q.z); st(a, OUZ_F_Q + 3, i, S.q.w);
-  st3(a, OUZ_F_V, i, S.v);
-  st3(a, OUZ_F_W, i, S.w);
-  sti(a, OUZ_I_PROGRESS, i, S.progress);
+  st3(S.T, OUZ_F_P, S.p);
+  st(S.T, OUZ_F_Q, S.q.x); st(S.T, OUZ_F_Q + 1, S.q.y); st(S.T, OUZ_F_Q + 2, S.q.z); st(S.T, OUZ_F_Q + 3, S.q.w);
+  st3(S.T, OUZ_F_V, S.v);
+  st3(S.T, OUZ_F_W, S.w);
+  sti(S.T, OUZ_I_PROGRESS, S.progress);
   if (a.track_episodes) {
-    st(a, OUZ_F_EP_RET, i, S.ep_ret);
+    st(S.T, OUZ_F_EP_RET, S.ep_ret);
     if (S.ep_cnt_add) {
-      st(a, OUZ_F_EP_SUM, i, ld(a, OUZ_F_EP_SUM, i) + S.ep_sum_add);
-      sti(a, OUZ_I_EP_CNT, i, ldi(a, OUZ_I_EP_CNT, i) + S.ep_cnt_add);
+      st(S.T, OUZ_F_EP_SUM, ld(S.T, OUZ_F_EP_SUM) + S.ep_sum_add);
+      sti(S.T, OUZ_I_EP_CNT, ldi(S.T, OUZ_I_EP_CNT) + S.ep_cnt_add);
     }
   }
-  if (S.landings_add) sti(a, OUZ_I_LANDINGS, i, ldi(a, OUZ_I_LANDINGS, i) + S.landings_add);
-  if (S.dirty & D_LAND) sti(a, OUZ_I_LAND_FLAG, i, S.land_flag);
-  if (S.dirty & D_DR) { st(a, OUZ_F_DR, i, S.dr_m); st(a, OUZ_F_DR + 1, i, S.dr_i); st(a, OUZ_F_DR + 2, i, S.dr_t); }
-  if constexpr (TGT == TGT_GOAL) st3(a, OUZ_F_TARGET, i, S.target);
+  if (S.landings_add) sti(S.T, OUZ_I_LANDINGS, ldi(S.T, OUZ_I_LANDINGS) + S.landings_add);
+  if (S.dirty & D_LAND) sti(S.T, OUZ_I_LAND_FLAG, S.land_flag);
+  if (S.dirty & D_DR) { st(S.T, OUZ_F_DR, S.dr_m); st(S.T, OUZ_F_DR + 1, S.dr_i); st(S.T, OUZ_F_DR + 2, S.dr_t); }
+  if constexpr (TGT == TGT_GOAL) st3(S.T, OUZ_F_TARGET, S.target);
   if constexpr (CTRL == CTRL_RL) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) st(a, OUZ_F_THRUST + k, i, S.thrust[k]);
-    if (S.dirty & D_FAULT) { sti(a, OUZ_I_FAULT_ROTOR, i, S.frot); sti(a, OUZ_I_FAULT_ONSET, i, S.fonset); st(a, OUZ_F_FAULT_ETA, i, S.eta); }
+    for (int k = 0; k < 4; ++k) st(S.T, OUZ_F_THRUST + k, S.thrust[k]);
+    if (S.dirty & D_FAULT) { sti(S.T, OUZ_I_FAULT_ROTOR, S.frot); sti(S.T, OUZ_I_FAULT_ONSET, S.fonset); st(S.T, OUZ_F_FAULT_ETA, S.eta); }
   }
   if constexpr (CTRL == CTRL_LEE_EST) {
-    st3(a, OUZ_F_PREV_V, i, S.prev_v);
-    st3(a, OUZ_F_WAYPOINT, i, S.wp);
-    st(a, OUZ_F_EKF_Q, i, S.eq.w); st(a, OUZ_F_EKF_Q + 1, i, S.eq.x); st(a, OUZ_F_EKF_Q + 2, i, S.eq.y); st(a, OUZ_F_EKF_Q + 3, i, S.eq.z);
+    st3(S.T, OUZ_F_PREV_V, S.prev_v);
+    st3(S.T, OUZ_F_WAYPOINT, S.wp);
+    st(S.T, OUZ_F_EKF_Q, S.eq.w); st(S.T, OUZ_F_EKF_Q + 1, S.eq.x); st(S.T, OUZ_F_EKF_Q + 2, S.eq.y); st(S.T, OUZ_F_EKF_Q + 3, S.eq.z);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) st(a, OUZ_F_EKF_P + k, i, S.eP[k]);
+    for (int k = 0; k < 10; ++k) st(S.T, OUZ_F_EKF_P + k, S.eP[k]);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_X + k, i, S.px[k]);
+    for (int k = 0; k < 9; ++k) st(S.T, OUZ_F_PV_X + k, S.px[k]);
 #pragma unroll
-    for (int k = 0; k < 45; ++k) st(a, OUZ_F_PV_P + k, i, S.pP[k]);
+    for (int k = 0; k < 45; ++k) st(S.T, OUZ_F_PV_P + k, S.pP[k]);
   }
   if constexpr (TGT == TGT_TRAJ) {
-    st(a, OUZ_F_PLAT, i, S.plat.x); st(a, OUZ_F_PLAT + 1, i, S.plat.y);
-    sti(a, OUZ_I_TRAJ_IDX, i, S.tidx);
-    if (S.dirty & D_TRAJ) { sti(a, OUZ_I_TRAJ_TYPE, i, S.ttype); st(a, OUZ_F_TRAJ_SD, i, S.sd); }
+    st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y);
+    sti(S.T, OUZ_I_TRAJ_IDX, S.tidx);
+    if (S.dirty & D_TRAJ) { sti(S.T, OUZ_I_TRAJ_TYPE, S.ttype); st(S.T, OUZ_F_TRAJ_SD, S.sd); }
   }
 }
 
@@ -298,7 +325,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     S.v = v3(0.0f, 0.0f, 0.0f);
     S.w = v3(0.0f, 0.0f, 0.0f);
     S.progress = 0;
-    if (S.land_flag < 0) S.land_flag = ldi(a, OUZ_I_LAND_FLAG, i);   // landing counter (ekf_lee_landed.py:323-331)
+    if (S.land_flag < 0) S.land_flag = ldi(S.T, OUZ_I_LAND_FLAG);   // landing counter (ekf_lee_landed.py:323-331)
     if (S.land_flag) { S.landings_add += S.land_flag; S.land_flag = 0; S.dirty |= D_LAND; }
     if (tp.dr) {
       U4 d = draw(a.seed, gid, sc.step, RNG_DR);
@@ -327,7 +354,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
                   __fadd_rn(unit_f32(r.z), 1.0f));
     }
-    float4 act = reinterpret_cast<const float4*>(sc.actions)[i];
+    float4 act = reinterpret_cast<const float4*>(sc.actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
     float av[4] = {act.x, act.y, act.z, act.w};
     float eff[4];
     const bool on = tp.fault && S.progress >= S.fonset;
@@ -517,8 +544,8 @@ struct OutPtrs {
 
 __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, int n, bool valid, const float* ob,
                                      float rew, bool rs, bool to, bool direct) {
-  const int lane = threadIdx.x & 63;
-  const int first = i - lane;
+  const uint32_t lane = (uint32_t)i & 63u;
+  const uint32_t first = wave_tile(i) * 64u;   // wave-uniform: output bases live in SGPRs
   if (direct) {   // wave shared by two tasks (misaligned mixed shard): plain per-lane stores
     if (valid) {
 #pragma unroll
@@ -532,17 +559,24 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
   if (valid) {
 #pragma unroll
     for (int k = 0; k < OUZ_NUM_OBS; ++k) wave_lds[lane * OUZ_NUM_OBS + k] = ob[k];
-    o.rew[i] = rew;
-    o.reset[i] = rs ? 1 : 0;
-    o.timeouts[i] = to ? 1 : 0;
+    (o.rew + first)[lane] = rew;
+    (o.reset + first)[lane] = rs ? 1 : 0;
+    (o.timeouts + first)[lane] = to ? 1 : 0;
   }
   wave_lds_sync();
-  const int m = min(64, n - first);
-  const int nf = m * OUZ_NUM_OBS;
+  const uint32_t m = min(64u, (uint32_t)(n - (int)first));
   float* dst = o.obs + (size_t)first * OUZ_NUM_OBS;   // 16-B aligned: waves start at multiples of 64 envs
   const float4* src4 = reinterpret_cast<const float4*>(wave_lds);
-  for (int k = lane; k < nf / 4; k += 64) reinterpret_cast<float4*>(dst)[k] = src4[k];
-  for (int k = (nf / 4) * 4 + lane; k < nf; k += 64) dst[k] = wave_lds[k];
+  float4* dst4 = reinterpret_cast<float4*>(dst);
+  if (m == 64) {   // full wave: 64 x 13 floats = 208 float4, 3.25 per lane
+#pragma unroll
+    for (uint32_t r = 0; r < 3; ++r) dst4[lane + 64u * r] = src4[lane + 64u * r];
+    if (lane < 16u) dst4[lane + 192u] = src4[lane + 192u];
+  } else {
+    const uint32_t nf = m * OUZ_NUM_OBS;
+    for (uint32_t k = lane; k < nf / 4; k += 64) dst4[k] = src4[k];
+    for (uint32_t k = (nf / 4) * 4 + lane; k < nf; k += 64) dst[k] = wave_lds[k];
+  }
   wave_lds_sync();
 }
 
@@ -555,12 +589,17 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   const TaskParams& tp = a.tp[task];
   const uint32_t gid = a.env_offset + (uint32_t)i;
   EnvRegs<CTRL, TGT> S;
+  S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
   if (valid) env_load<CTRL, TGT>(a, i, tp, S);
   if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
+#ifdef OUZ_PROBE_NOCORE
+    for (int k = 0; k < OUZ_NUM_OBS; ++k) ob[k] = S.p.x * k;
+#else
     if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
+#endif
     emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
   } else {
     for (int k = 0; k < K; ++k) {

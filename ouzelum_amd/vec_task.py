@@ -134,7 +134,9 @@ class QuadVecTask:
                 torch.cuda.synchronize(self.device)
             except Exception:  # noqa: BLE001
                 pass
-            L.lib.ouz_destroy(env)
+            lib = getattr(L, "lib", None)
+            if lib is not None:      # None during interpreter shutdown
+                lib.ouz_destroy(env)
             self._env = None
 
     # ------------------------------------------------------- VecTask surface
