@@ -213,6 +213,25 @@ int ouz_reward(const float* root13, const float* target, const int32_t* progress
 int ouz_philox(uint64_t seed, const uint32_t* env_ids, uint32_t step, uint32_t stream_id, uint32_t sub,
                uint32_t* out4, int32_t n, void* stream);
 
+/* ---- learner-side kernels (recurrent PPO/RPO on MI355X) ---- */
+
+/* Generalized advantage estimation over a (T, N) rollout (RPO-LSTM/agent.py:40-55,
+ * PPO/agent.py:40-55).  rewards/values/dones [T][N] f32 (dones[t] = done flag
+ * observed before step t), next_value/next_done [N] f32, outputs [T][N] f32.
+ * gamma_lam = f32(gamma * lambda) as the reference's Python scalar product.
+ * torch float32 operation order: bit-identical to the reference formula. */
+int ouz_gae(const float* rewards, const float* values, const float* dones, const float* next_value,
+            const float* next_done, int32_t T, int32_t N, float gamma, float gamma_lam, float* advantages,
+            float* returns, void* stream);
+
+/* POMDPWrapper.observation (utils/POMDP.py:23-43) applied by the learner to a
+ * (rows, dim) f32 batch (RPO-LSTM/main.py:103): flicker zeroes the whole batch
+ * with one coin per call, random_noise multiplies by U(1-prob, 1+prob) per
+ * element, flickering_and_random_noise = flicker p 0.1 then noise.  Draws are
+ * keyed (seed, row_offset + row, call); in == out is allowed. */
+int ouz_pomdp_obs(const float* in, float* out, int32_t rows, int32_t dim, int32_t mode, float prob, uint64_t seed,
+                  int64_t row_offset, uint32_t call, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,8 +9,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "quad_kernels.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc", "philox.h"),
+SRCS = [os.path.join(HERE, "csrc", "quad_kernels.hip"), os.path.join(HERE, "csrc", "learner_kernels.hip")]
+DEPS = [*SRCS, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc", "philox.h"),
         os.path.join(ROOT, "include", "ouzelum.h")]
 OUT = os.path.join(HERE, "libouzelum_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -18,7 +18,10 @@ ARCH = os.environ.get("OUZ_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          # f32 divide / sqrt to ~1-2 ulp instead of correctly rounded: -14 % VALU in the step kernel,
          # well inside the parity tolerances.  f64 (PV filter) and the RNG (__f*_rn) are unaffected.
-         "-fno-hip-fp32-correctly-rounded-divide-sqrt"]
+         "-fno-hip-fp32-correctly-rounded-divide-sqrt",
+         # FMA contraction stays on everywhere except where a `#pragma clang fp contract(off)` asks for
+         # torch's one-rounding-per-op order (RNG uniforms, GAE): __fmul_rn/__fadd_rn are plain operators in HIP.
+         "-ffp-contract=fast-honor-pragmas"]
 
 
 def up_to_date() -> bool:
@@ -32,7 +35,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
     extra = os.environ.get("OUZ_EXTRA_FLAGS", "").split()
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

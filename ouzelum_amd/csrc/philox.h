@@ -25,7 +25,8 @@ enum RngStream : uint32_t {
 };
 constexpr uint32_t BATCH_ENV = 0xFFFFFFFFu;
 constexpr uint32_t INIT_STEP = 0xFFFFFFFFu;
-enum PomdpSite : uint32_t { SITE_OBS = 0, SITE_GYR = 1, SITE_ANG = 2, SITE_ACC = 3, SITE_POS = 4, SITE_VEL = 5 };
+enum PomdpSite : uint32_t { SITE_OBS = 0, SITE_GYR = 1, SITE_ANG = 2, SITE_ACC = 3, SITE_POS = 4, SITE_VEL = 5,
+                            SITE_LEARNER = 6 /* learner-side POMDPWrapper (RPO-LSTM/main.py:103) */ };
 
 struct U4 { uint32_t x, y, z, w; };
 
@@ -58,8 +59,9 @@ OUZ_HD float unit_f32(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f
 // lo + (hi - lo) * u with each op rounded separately (no FMA contraction), so the
 // CPU oracle's float32 numpy expression gives the same bits.
 OUZ_HD float uniform_f32(uint32_t x, float lo, float hi) {
+#pragma clang fp contract(off)   // two roundings, never an FMA (the oracle's numpy order)
 #if defined(__HIP_DEVICE_COMPILE__)
-  return __fadd_rn(lo, __fmul_rn(__fsub_rn(hi, lo), unit_f32(x)));
+  return lo + (hi - lo) * unit_f32(x);
 #else
   volatile float span = hi - lo;
   volatile float m = span * unit_f32(x);

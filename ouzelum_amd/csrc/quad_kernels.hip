@@ -913,6 +913,9 @@ inline int block_for(int n) { return n <= 65536 ? 64 : 256; }
   } while (0)
 }  // namespace
 
+// shared with learner_kernels.hip (one ouz_last_error for the whole library)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+
 struct ouz_env {
   ouz_config cfg;
   ouz_buffers buf;

@@ -1,0 +1,132 @@
+"""Policy / value networks of the reference learners, re-laid for MI355X.
+
+Same architectures and parameter names as ``RPO-LSTM/model.py:11-84`` and
+``PPO/model.py:11-55`` (so the reference's ``*_actor`` / ``*_critic`` state dicts
+load unchanged), with the recurrent actor restructured for the GPU:
+
+* ``LSTMActor.get_states`` (reference ``model.py:34-50``) calls ``nn.LSTM`` once
+  per time step because the done mask resets the carry between steps.  Here the
+  input projection ``x W_ihᵀ + b_ih + b_hh`` of all T steps is one GEMM over
+  (T·B, 256) — hipBLASLt at a useful size — and only the (B,128)x(128,512)
+  recurrent product plus the gate nonlinearities remain per step.  Gate order
+  and arithmetic are torch's LSTM cell (i, f, g, o).
+* RPO's policy-update noise ``z ~ U(-alpha, alpha)`` (``model.py:61-64``) is drawn
+  on the actor's device instead of a CPU ``FloatTensor`` copied to ``cuda:0``.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.distributions.normal import Normal
+
+
+def layer_init(layer, std=math.sqrt(2), bias_const=0.0):
+    """Orthogonal weights, constant bias (model.py:6-9)."""
+    torch.nn.init.orthogonal_(layer.weight, std)
+    torch.nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+def _flat(space):
+    return int(np.prod(space.shape))
+
+
+class MLPActor(nn.Module):
+    """PPO actor: 13 -> 256 -> 256 -> 4 tanh MLP mean + state-independent log-std (PPO/model.py:11-40)."""
+
+    def __init__(self, observation_space, action_space, rpo_alpha=0.0):
+        super().__init__()
+        self.rpo_alpha = rpo_alpha
+        n_obs, n_act = _flat(observation_space), _flat(action_space)
+        self.actor_mean = nn.Sequential(
+            layer_init(nn.Linear(n_obs, 256)), nn.Tanh(),
+            layer_init(nn.Linear(256, 256)), nn.Tanh(),
+            layer_init(nn.Linear(256, n_act), std=0.01),
+        )
+        self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+
+    def forward(self, state, action=None):
+        mean = self.actor_mean(state)
+        return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha)
+
+
+class LSTMActor(nn.Module):
+    """RPO-LSTM actor (RPO-LSTM/model.py:11-70): 13 -> 512 -> 256 tanh trunk, LSTM(256, 128),
+    linear mean head, state-independent log-std, RPO alpha 0.5."""
+
+    def __init__(self, observation_space, action_space, rpo_alpha=0.5, hidden=128):
+        super().__init__()
+        self.rpo_alpha = rpo_alpha
+        n_obs, n_act = _flat(observation_space), _flat(action_space)
+        self.network = nn.Sequential(
+            layer_init(nn.Linear(n_obs, 512)), nn.Tanh(),
+            layer_init(nn.Linear(512, 256)), nn.Tanh(),
+        )
+        self.lstm = nn.LSTM(256, hidden)
+        for name, param in self.lstm.named_parameters():
+            if "bias" in name:
+                nn.init.constant_(param, 0)
+            elif "weight" in name:
+                nn.init.orthogonal_(param, 1.0)
+        self.actor_mean = layer_init(nn.Linear(hidden, n_act), std=0.01)
+        self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+
+    def initial_state(self, num_envs, device):
+        shape = (self.lstm.num_layers, num_envs, self.lstm.hidden_size)
+        return torch.zeros(shape, device=device), torch.zeros(shape, device=device)
+
+    def get_states(self, state, lstm_state, done):
+        """(T·B, obs) trunk features -> (T·B, H) LSTM outputs; the carry of env b is zeroed
+        before step t when done[t, b] (model.py:34-50).  Returns (hidden, (h, c))."""
+        feats = self.network(state)
+        h, c = lstm_state
+        B = h.shape[1]
+        H = self.lstm.hidden_size
+        x_proj = torch.addmm(self.lstm.bias_ih_l0 + self.lstm.bias_hh_l0, feats, self.lstm.weight_ih_l0.t())
+        x_proj = x_proj.view(-1, B, 4 * H)
+        keep = (1.0 - done).view(-1, B, 1)
+        h, c = h[0], c[0]
+        w_hh_t = self.lstm.weight_hh_l0.t()
+        outs = []
+        for t in range(x_proj.shape[0]):
+            h = keep[t] * h
+            c = keep[t] * c
+            gates = torch.addmm(x_proj[t], h, w_hh_t)
+            i, f, g, o = gates.chunk(4, dim=1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            outs.append(h)
+        return torch.cat(outs, 0), (h.unsqueeze(0), c.unsqueeze(0))
+
+    def forward(self, state, lstm_state, done, action=None):
+        hidden, lstm_state = self.get_states(state, lstm_state, done)
+        mean = self.actor_mean(hidden)
+        return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha), lstm_state)
+
+
+def _policy_head(mean, logstd, action, rpo_alpha):
+    std = torch.exp(logstd.expand_as(mean))
+    if action is None:
+        probs = Normal(mean, std)
+        action = probs.sample()
+    else:
+        if rpo_alpha > 0.0:   # RPO: perturb the mean for the policy update (RPO-LSTM/model.py:61-64)
+            mean = mean + torch.empty_like(mean).uniform_(-rpo_alpha, rpo_alpha)
+        probs = Normal(mean, std)
+    return action, probs.log_prob(action).sum(1), probs.entropy().sum(1)
+
+
+class Critic(nn.Module):
+    """Value MLP 13 -> 256 -> 256 -> 1 (RPO-LSTM/model.py:72-84)."""
+
+    def __init__(self, observation_space):
+        super().__init__()
+        self.critic = nn.Sequential(
+            layer_init(nn.Linear(_flat(observation_space), 256)), nn.Tanh(),
+            layer_init(nn.Linear(256, 256)), nn.Tanh(),
+            layer_init(nn.Linear(256, 1), std=1.0),
+        )
+
+    def forward(self, state):
+        return self.critic(state)

@@ -1,0 +1,166 @@
+"""PPO / RPO-LSTM update on MI355X with the rollout size as a parameter.
+
+Mirrors ``RPO-LSTM/agent.py:9-147`` (recurrent, env-wise minibatches, RPO noise) and
+``PPO/agent.py`` (feed-forward, sample-wise minibatches): same hyper-parameters
+(clip 0.2, gamma 0.99, lambda 0.95, 4 epochs, 2 minibatches, vf_coef 2, grad-norm 1,
+Adam lr 2.6e-3 eps 1e-5, advantage normalisation) and the same checkpoint files.
+Differences, all MI355X-side:
+
+* N and T are parameters: the reference hard-codes ``values.reshape(16, 4096)``
+  (``agent.py:61``), so any other env count crashes there.
+* GAE is one HIP launch (``ouz_gae``) instead of a T-step Python loop; values are
+  computed without building an autograd graph (the reference's graph there is
+  never used: ``clip_vloss`` is False).
+* Minibatch permutations come from ``torch.randperm`` on the device (no H2D copy of
+  a numpy permutation) and the clip fractions stay on the device until the end of
+  the update (the reference syncs with ``.item()`` every minibatch).
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib as L
+from .models import Critic, LSTMActor, MLPActor
+
+
+def gae(rewards, values, dones, next_value, next_done, gamma=0.99, lam=0.95):
+    """(returns, advantages), each (T, N) f32, from the HIP kernel (RPO-LSTM/agent.py:40-55)."""
+    T, N = rewards.shape
+    ts = [t.contiguous().float() for t in (rewards, values, dones, next_value.reshape(N), next_done.reshape(N))]
+    for t, name in zip(ts, ("rewards", "values", "dones", "next_value", "next_done")):
+        L.require_hip_tensor(t, name)
+    adv = torch.empty_like(ts[0])
+    ret = torch.empty_like(ts[0])
+    # the reference multiplies by the Python product gamma * lambda (a double), rounded once to f32
+    L.check(L.lib.ouz_gae(*(L.ptr(t) for t in ts), T, N, gamma, float(gamma * lam), L.ptr(adv), L.ptr(ret),
+                          L.stream_ptr(adv.device)), "ouz_gae")
+    return ret, adv
+
+
+class PPOLearner:
+    def __init__(self, observation_space, action_space, num_envs, device, recurrent=True, rollout_steps=16,
+                 lr=0.0026, num_minibatches=2, update_epochs=4):
+        self.obs_dim = observation_space
+        self.act_dim = action_space
+        self.num_envs = num_envs
+        self.rollout_steps = rollout_steps
+        self.device = torch.device(device)
+        self.recurrent = recurrent
+        self.clip_coef = 0.2
+        self.gamma = 0.99
+        self.gae_lamda = 0.95
+        self.norm_adv = True
+        self.update_epochs = update_epochs
+        self.ent_coef = 0.0
+        self.vf_coef = 2
+        self.clip_vloss = False
+        self.target_kl = None
+        self.max_grad_norm = 1
+        self.num_minibatches = num_minibatches
+        self.batch_size = num_envs * rollout_steps
+        self.minibatch_size = self.batch_size // num_minibatches
+        if recurrent and num_envs % num_minibatches:
+            raise ValueError("num_envs must divide into the minibatches")   # agent.py:72
+        self.actor = (LSTMActor(observation_space, action_space) if recurrent
+                      else MLPActor(observation_space, action_space)).to(self.device)
+        self.critic = Critic(observation_space).to(self.device)
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr, eps=1e-5)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=lr, eps=1e-5)
+
+    # ------------------------------------------------------------------ rollout
+    @torch.no_grad()
+    def get_action(self, state, lstm_state=None, done=None):
+        if self.recurrent:
+            return self.actor(state, lstm_state, done)
+        return (*self.actor(state), None)
+
+    def initial_state(self):
+        return self.actor.initial_state(self.num_envs, self.device) if self.recurrent else None
+
+    @torch.no_grad()
+    def get_gae(self, next_obs, next_done, rewards, dones, values):
+        next_value = self.critic(next_obs).reshape(-1)
+        return gae(rewards, values, dones, next_value, next_done, self.gamma, self.gae_lamda)
+
+    # ------------------------------------------------------------------- update
+    def train(self, obs, pomdps, actions, next_obs, next_done, initial_lstm_state, logprobs, rewards, dones):
+        """One PPO update on a (T, N) rollout.  ``pomdps`` are the observations the actor trains on
+        (RPO-LSTM trains on the POMDP-corrupted ones, agent.py:83); pass ``obs`` for plain PPO."""
+        T, N = rewards.shape
+        with torch.no_grad():
+            values = self.critic(obs.reshape(T * N, -1)).reshape(T, N)
+        returns, advantages = self.get_gae(next_obs, next_done, rewards, dones, values)
+        b_obs = obs.reshape(T * N, -1)
+        b_pomdps = pomdps.reshape(T * N, -1)
+        b_actions = actions.reshape(T * N, -1)
+        b_logprobs = logprobs.reshape(-1)
+        b_dones = dones.reshape(-1)
+        b_advantages = advantages.reshape(-1)
+        b_returns = returns.reshape(-1)
+        flatinds = torch.arange(T * N, device=self.device).reshape(T, N)
+        clipfracs = torch.zeros((), device=self.device)
+        n_mb = 0
+        stats = {}
+        for _ in range(self.update_epochs):
+            if self.recurrent:
+                envinds = torch.randperm(N, device=self.device)
+                per = N // self.num_minibatches
+                batches = [(flatinds[:, envinds[s:s + per]].reshape(-1), envinds[s:s + per])
+                           for s in range(0, N, per)]
+            else:
+                b_inds = torch.randperm(T * N, device=self.device)
+                batches = [(b_inds[s:s + self.minibatch_size], None) for s in range(0, T * N, self.minibatch_size)]
+            for mb_inds, mbenvinds in batches:
+                if self.recurrent:
+                    _, newlogprob, entropy, _ = self.actor(
+                        b_pomdps[mb_inds], (initial_lstm_state[0][:, mbenvinds], initial_lstm_state[1][:, mbenvinds]),
+                        b_dones[mb_inds], b_actions[mb_inds])
+                else:
+                    _, newlogprob, entropy = self.actor(b_pomdps[mb_inds], b_actions[mb_inds])
+                newvalue = self.critic(b_obs[mb_inds]).view(-1)
+                logratio = newlogprob - b_logprobs[mb_inds]
+                ratio = logratio.exp()
+                with torch.no_grad():
+                    approx_kl = ((ratio - 1) - logratio).mean()
+                    clipfracs += ((ratio - 1.0).abs() > self.clip_coef).float().mean()
+                    n_mb += 1
+                mb_adv = b_advantages[mb_inds]
+                if self.norm_adv:
+                    mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
+                pg_loss = torch.max(-mb_adv * ratio,
+                                    -mb_adv * torch.clamp(ratio, 1 - self.clip_coef, 1 + self.clip_coef)).mean()
+                v_loss = 0.5 * ((newvalue - b_returns[mb_inds]) ** 2).mean()
+                actor_loss = pg_loss - self.ent_coef * entropy.mean()
+                critic_loss = v_loss * self.vf_coef
+
+                self.actor_optimizer.zero_grad()
+                actor_loss.backward()
+                nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad_norm)
+                self.actor_optimizer.step()
+
+                self.critic_optimizer.zero_grad()
+                critic_loss.backward()
+                nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad_norm)
+                self.critic_optimizer.step()
+                stats = {"pg_loss": pg_loss.detach(), "v_loss": v_loss.detach(), "approx_kl": approx_kl}
+            if self.target_kl is not None and float(stats["approx_kl"]) > self.target_kl:
+                break
+        stats["clipfrac"] = clipfracs / max(n_mb, 1)
+        return stats
+
+    # -------------------------------------------------------------- checkpoints
+    def save(self, filename):
+        """Same four files as agent.py:127-131."""
+        torch.save(self.critic.state_dict(), filename + "_critic")
+        torch.save(self.critic_optimizer.state_dict(), filename + "_critic_optimizer")
+        torch.save(self.actor.state_dict(), filename + "_actor")
+        torch.save(self.actor_optimizer.state_dict(), filename + "_actor_optimizer")
+
+    def load(self, filename):
+        """agent.py:133-139; tensors only (weights_only)."""
+        m = self.device
+        self.critic.load_state_dict(torch.load(filename + "_critic", map_location=m, weights_only=True))
+        self.critic_optimizer.load_state_dict(torch.load(filename + "_critic_optimizer", map_location=m,
+                                                         weights_only=True))
+        self.actor.load_state_dict(torch.load(filename + "_actor", map_location=m, weights_only=True))
+        self.actor_optimizer.load_state_dict(torch.load(filename + "_actor_optimizer", map_location=m,
+                                                        weights_only=True))

@@ -21,6 +21,10 @@ and writes small ``.npz`` fixtures next to itself.  The fixtures are data
 * Trajectories  isaacgymenvs/utils/trajectories.py.
 * Quaternion rotate (xyzw)  isaacgymenvs/tasks/amp/poselib/poselib/core/rotation3d.py
   (quat_rotate) — the importable twin of isaacgym.torch_utils.quat_rotate.
+* Learner  isaacgymenvs/RPO-LSTM/{model,agent}.py — ``PPO.getGAE`` run unbound on a
+  stub ``self`` (critic = fixed next values), and the LSTM actor's ``get_states`` /
+  ``actor_mean`` / critic forward with the module's own seeded initialisation
+  (parameters saved by their state_dict names).  Only CPU paths run.
 """
 import argparse
 import importlib.util
@@ -244,6 +248,51 @@ def gen_traj_and_quat(ref):
     np.savez_compressed(os.path.join(HERE, "traj_quat.npz"), **out)
 
 
+def gen_learner(ref):
+    d = os.path.join(ref, "isaacgymenvs", "RPO-LSTM")
+    model = _load("model", os.path.join(d, "model.py"))      # agent.py does `from model import ...`
+    agent = _load("ref_rpo_agent", os.path.join(d, "agent.py"))
+    rs = np.random.RandomState(5000)
+    T, N = 16, 37
+    rew = rs.normal(0.5, 1.0, (T, N)).astype(np.float32)
+    val = rs.normal(0.0, 2.0, (T, N)).astype(np.float32)
+    done = (rs.uniform(0, 1, (T, N)) < 0.15).astype(np.float32)
+    next_val = rs.normal(0.0, 2.0, (N,)).astype(np.float32)
+    next_done = (rs.uniform(0, 1, (N,)) < 0.15).astype(np.float32)
+    nv_t = torch.tensor(next_val)
+    stub = types.SimpleNamespace(critic=lambda obs: nv_t.reshape(-1, 1), rollout_steps=T, gamma=0.99,
+                                 gae_lamda=0.95, device="cpu")
+    ret, adv = agent.PPO.getGAE(stub, torch.zeros(N, 13), torch.tensor(next_done), torch.tensor(rew),
+                                torch.tensor(done), torch.tensor(val))
+    out = {"gae_rewards": rew, "gae_values": val, "gae_dones": done, "gae_next_value": next_val,
+           "gae_next_done": next_done, "gae_returns": ret.numpy(), "gae_advantages": adv.numpy()}
+
+    class Space:
+        def __init__(self, shape):
+            self.shape = shape
+
+    torch.manual_seed(7)
+    actor = model.Actor(Space((13,)), Space((4,)))
+    critic = model.Critic(Space((13,)))
+    B, Tl = 11, 6
+    x = torch.tensor(rs.normal(0, 1, (Tl * B, 13)).astype(np.float32))
+    dn = torch.tensor((rs.uniform(0, 1, (Tl * B,)) < 0.2).astype(np.float32))
+    h0 = torch.tensor(rs.normal(0, 0.5, (1, B, 128)).astype(np.float32))
+    c0 = torch.tensor(rs.normal(0, 0.5, (1, B, 128)).astype(np.float32))
+    with torch.no_grad():
+        hid, (h1, c1) = actor.get_states(x, (h0, c0), dn)
+        mean = actor.actor_mean(hid)
+        v = critic(x)
+    out.update({"lstm_x": x.numpy(), "lstm_done": dn.numpy(), "lstm_h0": h0.numpy(), "lstm_c0": c0.numpy(),
+                "lstm_hidden": hid.numpy(), "lstm_h1": h1.numpy(), "lstm_c1": c1.numpy(),
+                "actor_mean_out": mean.numpy(), "critic_out": v.numpy()})
+    for k, t in actor.state_dict().items():
+        out["actor." + k] = t.numpy()
+    for k, t in critic.state_dict().items():
+        out["critic." + k] = t.numpy()
+    np.savez_compressed(os.path.join(HERE, "learner.npz"), **out)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -252,4 +301,5 @@ if __name__ == "__main__":
     gen_ekf(a.ref)
     gen_pv(a.ref)
     gen_traj_and_quat(a.ref)
+    gen_learner(a.ref)
     print("golden fixtures written to", HERE)

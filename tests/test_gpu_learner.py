@@ -1,0 +1,94 @@
+"""Learner kernels and the recurrent training loop on the GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner_oracle as LO
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gae_kernel_bit_exact(golden):
+    from ouzelum_amd.learners import gae
+    lg = golden("learner.npz")
+    dev = "cuda"
+    ret, adv = gae(*(torch.tensor(lg[k], device=dev) for k in ("gae_rewards", "gae_values", "gae_dones",
+                                                                "gae_next_value", "gae_next_done")))
+    np.testing.assert_array_equal(adv.cpu().numpy(), lg["gae_advantages"])     # reference getGAE, f32
+    np.testing.assert_array_equal(ret.cpu().numpy(), lg["gae_returns"])
+    # a rollout of the bench shape against the oracle
+    rs = np.random.RandomState(3)
+    T, N = 16, 4096 + 37
+    r, v = rs.normal(0, 1, (T, N)).astype(np.float32), rs.normal(0, 3, (T, N)).astype(np.float32)
+    d = (rs.uniform(0, 1, (T, N)) < 0.1).astype(np.float32)
+    nv, nd = rs.normal(0, 3, N).astype(np.float32), (rs.uniform(0, 1, N) < 0.1).astype(np.float32)
+    ret, adv = gae(*(torch.tensor(x, device=dev) for x in (r, v, d, nv, nd)))
+    oret, oadv = LO.gae_f32(r, v, d, nv, nd)
+    np.testing.assert_array_equal(adv.cpu().numpy(), oadv)
+    np.testing.assert_array_equal(ret.cpu().numpy(), oret)
+
+
+@pytest.mark.parametrize("mode,name", [(1, "flicker"), (2, "random_noise"), (3, "flickering_and_random_noise")])
+def test_pomdp_obs_kernel_bit_exact(mode, name):
+    from ouzelum_amd.learners import POMDPWrapper
+    rs = np.random.RandomState(mode)
+    x = rs.normal(0, 1, (1000, 13)).astype(np.float32)
+    w = POMDPWrapper(name, 0.3, seed=21, row_offset=500)
+    xt = torch.tensor(x, device="cuda")
+    for call in range(12):
+        y = w.observation(xt)
+        np.testing.assert_array_equal(y.cpu().numpy(), LO.pomdp_obs(x, mode, 0.3, 21, 500, call))
+    # in place is allowed
+    w2 = POMDPWrapper(name, 0.3, seed=21, row_offset=500)
+    z = xt.clone()
+    w2.observation(z, out=z)
+    np.testing.assert_array_equal(z.cpu().numpy(), LO.pomdp_obs(x, mode, 0.3, 21, 500, 0))
+
+
+def test_lstm_actor_gpu_matches_nn_lstm_loop():
+    """The one-GEMM input projection equals the reference's per-step nn.LSTM loop (model.py:34-50)."""
+    from ouzelum_amd.learners.models import LSTMActor
+    from ouzelum_amd.spaces import Box
+    torch.manual_seed(0)
+    a = LSTMActor(Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))).cuda()
+    T, B = 16, 256
+    x = torch.randn(T * B, 13, device="cuda")
+    dn = (torch.rand(T * B, device="cuda") < 0.1).float()
+    h0 = torch.randn(1, B, 128, device="cuda") * 0.5
+    c0 = torch.randn(1, B, 128, device="cuda") * 0.5
+    with torch.no_grad():
+        hid, (h1, c1) = a.get_states(x, (h0, c0), dn)
+        feats = a.network(x).reshape(T, B, 256)
+        st = (h0, c0)
+        outs = []
+        for t in range(T):
+            keep = (1.0 - dn.reshape(T, B)[t]).view(1, -1, 1)
+            o, st = a.lstm(feats[t].unsqueeze(0), (keep * st[0], keep * st[1]))
+            outs.append(o)
+        ref = torch.flatten(torch.cat(outs), 0, 1)
+    torch.testing.assert_close(hid, ref, atol=5e-5, rtol=1e-4)
+    torch.testing.assert_close(h1, st[0], atol=5e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("algo,env,n", [("rpo_lstm", "EKFLeeLanded", 1000), ("ppo", "Ouzelum", 512)])
+def test_training_loop_runs(tmp_path, algo, env, n):
+    """The reference loop with N != 4096 (the reference hard-codes reshape(16, 4096), agent.py:61)."""
+    from ouzelum_amd.learners.train import main
+    out = main(["--algo", algo, "--env", env, "--num_envs", str(n), "--total_steps", str(n * 16 * 3),
+                "--logdir", str(tmp_path / "runs"), "--checkpoint_dir", str(tmp_path / "ck"), "--quiet"])
+    h = out["history"]
+    assert len(h) == 3
+    for row in h:
+        for k in ("average_reward", "pg_loss", "v_loss", "approx_kl"):
+            assert np.isfinite(row[k]), (k, row)
+    name = ("RPO_LSTM" if algo == "rpo_lstm" else "PPO") + "_flicker_0.1"
+    assert (tmp_path / "runs" / f"{name}.csv").exists()
+    assert (tmp_path / "ck" / f"{name}_actor").exists()
+    # checkpoint round trip (agent.py:127-139), tensors only
+    agent = out["agent"]
+    before = {k: v.clone() for k, v in agent.actor.state_dict().items()}
+    for p in agent.actor.parameters():
+        p.data.zero_()
+    agent.load(str(tmp_path / "ck" / name))
+    for k, v in agent.actor.state_dict().items():
+        assert torch.equal(v, before[k])

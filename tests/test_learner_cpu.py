@@ -1,0 +1,87 @@
+"""Learner pieces that run without a GPU: the GAE oracle against the reference's own getGAE
+(tests/golden/learner.npz), and the re-laid LSTM actor / critic against the reference modules'
+outputs with the reference's parameters loaded by their state_dict names."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import learner_oracle as LO
+from ouzelum_amd.learners.models import Critic, LSTMActor, MLPActor
+from ouzelum_amd.spaces import Box
+
+
+@pytest.fixture(scope="module")
+def lg(golden):
+    return golden("learner.npz")
+
+
+def _spaces():
+    return Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))
+
+
+def test_gae_oracle_bit_exact_vs_reference(lg):
+    ret, adv = LO.gae_f32(lg["gae_rewards"], lg["gae_values"], lg["gae_dones"], lg["gae_next_value"],
+                          lg["gae_next_done"])
+    np.testing.assert_array_equal(adv, lg["gae_advantages"])
+    np.testing.assert_array_equal(ret, lg["gae_returns"])
+
+
+def _load(module, lg, prefix):
+    sd = {k[len(prefix):]: torch.tensor(lg[k]) for k in lg.files if k.startswith(prefix)}
+    module.load_state_dict(sd, strict=True)
+    return module
+
+
+def test_parameter_names_match_reference(lg):
+    obs_s, act_s = _spaces()
+    ref_actor = {k[len("actor."):] for k in lg.files if k.startswith("actor.")}
+    ref_critic = {k[len("critic."):] for k in lg.files if k.startswith("critic.")}
+    assert set(LSTMActor(obs_s, act_s).state_dict()) == ref_actor
+    assert set(Critic(obs_s).state_dict()) == ref_critic
+
+
+def test_lstm_actor_matches_reference(lg):
+    obs_s, act_s = _spaces()
+    actor = _load(LSTMActor(obs_s, act_s), lg, "actor.")
+    critic = _load(Critic(obs_s), lg, "critic.")
+    with torch.no_grad():
+        hid, (h1, c1) = actor.get_states(torch.tensor(lg["lstm_x"]), (torch.tensor(lg["lstm_h0"]),
+                                                                       torch.tensor(lg["lstm_c0"])),
+                                         torch.tensor(lg["lstm_done"]))
+        mean = actor.actor_mean(hid)
+        v = critic(torch.tensor(lg["lstm_x"]))
+    # one GEMM for the input projection vs nn.LSTM per step: f32 reassociation only
+    np.testing.assert_allclose(hid.numpy(), lg["lstm_hidden"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(h1.numpy(), lg["lstm_h1"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(c1.numpy(), lg["lstm_c1"], atol=2e-6, rtol=1e-5)
+    np.testing.assert_allclose(mean.numpy(), lg["actor_mean_out"], atol=1e-6, rtol=1e-5)
+    np.testing.assert_allclose(v.numpy(), lg["critic_out"], atol=1e-5, rtol=1e-5)
+
+
+def test_policy_heads():
+    obs_s, act_s = _spaces()
+    torch.manual_seed(0)
+    x = torch.randn(24, 13)
+    a, lp, ent = MLPActor(obs_s, act_s)(x)
+    assert a.shape == (24, 4) and lp.shape == (24,) and ent.shape == (24,)
+    actor = LSTMActor(obs_s, act_s)
+    h = actor.initial_state(8, "cpu")
+    a, lp, ent, (h1, c1) = actor(x, h, torch.zeros(24))
+    assert a.shape == (24, 4) and h1.shape == (1, 8, 128)
+    # RPO: with an action given the mean is perturbed by U(-0.5, 0.5): log-probs differ from the clean head
+    _, lp2, _, _ = actor(x, h, torch.zeros(24), a)
+    assert not torch.allclose(lp, lp2)
+
+
+def test_learner_pomdp_oracle_modes():
+    rs = np.random.RandomState(0)
+    x = rs.normal(0, 1, (300, 13)).astype(np.float32)
+    flick = [LO.pomdp_obs(x, 1, 0.3, 11, 0, c) for c in range(200)]
+    frac = np.mean([float(np.all(f == 0)) for f in flick])
+    assert 0.2 < frac < 0.4                                   # one coin per call, p = 0.3
+    assert all(np.all(f == 0) or np.array_equal(f, x) for f in flick)
+    y = LO.pomdp_obs(x, 2, 0.25, 11, 0, 0)
+    r = y / x
+    assert r.min() >= 0.75 - 1e-6 and r.max() <= 1.25 + 1e-6
+    # sharded rows draw what the unsharded run draws for the same global rows
+    np.testing.assert_array_equal(LO.pomdp_obs(x[100:], 2, 0.25, 11, 100, 0), y[100:])
