@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1
 export TMPDIR=/tmp
-for spec in "Ouzelum 64" "LeeLanded 4096" "EKFLeeLanded 4096" "QuadTracking 4096" "QuadFault 8192" "QuadMixed 4096" "LeeLanded 4194304" "QuadTracking 1048576"; do
+for spec in "Ouzelum 64" "LeeLanded 4096" "EKFLeeLanded 4096" "QuadTracking 4096" "QuadFault 8192" "QuadMixed 4096" "LeeLanded 16777216" "EKFLeeLanded 4194304" "QuadTracking 4194304"; do
   set -- $spec
   ST=1000; [ $2 -gt 100000 ] && ST=100
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profall_${TAG}_$1_$2" -o run --output-format csv -- \
@@ -14,4 +14,5 @@ for spec in "Ouzelum 64" "LeeLanded 4096" "EKFLeeLanded 4096" "QuadTracking 4096
   echo "prof $spec ok"
 done
 bash "$R/scripts/gpu_pmc.sh" $TAG LeeLanded 4096 300 && bash "$R/scripts/gpu_pmc.sh" $TAG LeeLanded 4194304 100 && \
-bash "$R/scripts/gpu_pmc.sh" $TAG QuadTracking 4096 300 && bash "$R/scripts/gpu_pmc.sh" $TAG QuadTracking 1048576 100
+bash "$R/scripts/gpu_pmc.sh" $TAG LeeLanded 16777216 50 && bash "$R/scripts/gpu_pmc.sh" $TAG QuadTracking 4096 300 && \
+bash "$R/scripts/gpu_pmc.sh" $TAG QuadTracking 4194304 50 && bash "$R/scripts/gpu_pmc.sh" $TAG EKFLeeLanded 4194304 50
