@@ -146,6 +146,7 @@ typedef struct ouz_config {
   float thrust_rate;        /* RL thrust action scale (2000, ouzelum.py:237)     */
   int32_t track_episodes;   /* 1: accumulate episodic return/count in-kernel
                                (PPO/utils.py:4-35 RecordEpisodeStatisticsTorch)  */
+  int32_t max_episode_length; /* env.maxEpisodeLength (cfg/task/<Task>.yaml); 0 -> task default */
 } ouz_config;
 
 typedef struct ouz_buffers {

@@ -520,7 +520,7 @@ class TaskSpec:
     motor_yaw: bool = False
 
 
-def task_spec(task, pomdp=None, pomdp_prob=None):
+def task_spec(task, pomdp=None, pomdp_prob=None, max_episode_length=0):
     if task == TASK_OUZELUM:      # tasks/ouzelum.py, cfg/task/Ouzelum.yaml
         s = TaskSpec(CTRL_RL, TGT_GOAL, 2000, 0.5, 0.0, False, 0.0)
     elif task == TASK_LEE_LANDED:  # tasks/lee_landed.py:25,263-330, cfg/task/LeeLanded.yaml
@@ -538,6 +538,8 @@ def task_spec(task, pomdp=None, pomdp_prob=None):
         s = replace(s, pomdp=pomdp)
     if pomdp_prob is not None:
         s = replace(s, pomdp_prob=pomdp_prob)
+    if max_episode_length:       # env.maxEpisodeLength from the task YAML
+        s = replace(s, max_episode_length=int(max_episode_length))
     return s
 
 
@@ -559,6 +561,7 @@ class EnvConfig:
     fault_eta_hi: float = 0.5
     thrust_max: float = 2000.0   # ouzelum.py:91
     thrust_rate: float = 2000.0  # ouzelum.py:237
+    max_episode_length: int = 0  # 0 -> task default
 
 
 def env_task_ids(cfg: EnvConfig):
@@ -584,7 +587,8 @@ class OracleEnv:
         self.n_total = cfg.num_envs_total or n
         self.gid = (cfg.env_id_offset + np.arange(n)).astype(np.int64)
         self.task_ids = env_task_ids(cfg)
-        self.specs = {t: task_spec(t, cfg.pomdp, cfg.pomdp_prob) for t in np.unique(self.task_ids)}
+        self.specs = {t: task_spec(t, cfg.pomdp, cfg.pomdp_prob, cfg.max_episode_length)
+                      for t in np.unique(self.task_ids)}
         self.sim_step = 0
         f = lambda *s: np.zeros((n,) + s, dtype=dtype)
         self.p, self.v, self.w = f(3), f(3), f(3)

@@ -51,6 +51,7 @@ class OuzConfig(ctypes.Structure):
         ("substeps", ctypes.c_int32), ("convergence_time", ctypes.c_int32), ("plat_speed", ctypes.c_float),
         ("dr_lo", ctypes.c_float), ("dr_hi", ctypes.c_float), ("fault_eta_hi", ctypes.c_float),
         ("thrust_max", ctypes.c_float), ("thrust_rate", ctypes.c_float), ("track_episodes", ctypes.c_int32),
+        ("max_episode_length", ctypes.c_int32),
     ]
 
 

@@ -985,6 +985,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   if (cfg->task < 0 || cfg->task >= OUZ_NUM_TASKS) return fail(OUZ_ERR_INVALID, "ouz_create: unknown task");
   if (cfg->num_envs <= 0) return fail(OUZ_ERR_INVALID, "ouz_create: num_envs must be > 0");
   if (cfg->substeps <= 0 || !(cfg->dt > 0.0f)) return fail(OUZ_ERR_INVALID, "ouz_create: bad dt/substeps");
+  if (cfg->max_episode_length < 0) return fail(OUZ_ERR_INVALID, "ouz_create: max_episode_length must be >= 0");
   int64_t total = cfg->num_envs_total > 0 ? cfg->num_envs_total : cfg->num_envs;
   if (cfg->env_id_offset < 0 || cfg->env_id_offset + cfg->num_envs > total || total > 0xFFFFFFFFll)
     return fail(OUZ_ERR_INVALID, "ouz_create: env ids out of range");
@@ -1034,6 +1035,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     TaskParams tp = task_preset(t);
     if (cfg->pomdp >= 0) tp.pomdp = cfg->pomdp;
     if (cfg->pomdp_prob >= 0.0f) tp.pomdp_prob = cfg->pomdp_prob;
+    if (cfg->max_episode_length > 0) tp.max_ep = cfg->max_episode_length;
     double prob = (double)tp.pomdp_prob;
     tp.noise_lo = (float)(1.0 - prob);
     tp.noise_hi = (float)(1.0 + prob);

@@ -40,6 +40,8 @@ def parse_args(argv=None):
     p.add_argument("--checkpoint_dir", default="checkpoints")
     p.add_argument("--no_checkpoints", action="store_true")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--play", action="store_true", help="run a saved policy (RPO-LSTM/play.py) instead of training")
+    p.add_argument("--checkpoint", default=None, help="checkpoint prefix (agent.save's filename)")
     return p.parse_args(argv)
 
 
@@ -130,8 +132,35 @@ def train(args):
             "env_steps_per_s": global_step / elapsed}
 
 
+@torch.no_grad()
+def play(args):
+    """RPO-LSTM/play.py:25-80: load a checkpoint and run the policy, printing the mean reward."""
+    device = torch.device("cuda", 0)
+    N = args.num_envs
+    base = make(seed=args.seed, task=args.env, num_envs=N, sim_device=str(device), rl_device=str(device),
+                track_episodes=True)
+    env = ExtractObsWrapper(base)
+    agent = PPOLearner(base.observation_space, base.action_space, N, device, recurrent=args.algo == "rpo_lstm",
+                       rollout_steps=args.rollout_steps)
+    if args.checkpoint:
+        agent.load(args.checkpoint)
+    next_obs = env.reset()
+    next_done = torch.zeros(N, device=device)
+    lstm = agent.initial_state()
+    rewards = []
+    for _ in range(max(1, args.total_steps // N)):
+        action, _, _, lstm = agent.get_action(next_obs, lstm, next_done)
+        next_obs, rew, next_done, _ = env.step(action)
+        rewards.append(rew.mean())
+        if not args.quiet:
+            print(f"Average rewards {float(rewards[-1]):.4f}")
+    return {"mean_reward": float(torch.stack(rewards).mean()), "episode_stats": base.episode_stats().tolist()}
+
+
 def main(argv=None):
     args = parse_args(argv)
+    if args.play:
+        return play(args)
     out = train(args)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -83,7 +83,7 @@ class QuadVecTask:
             setattr(cfg, k, v)
         self.cfg = cfg
         info = task_info(self.task)
-        self.max_episode_length = info.max_episode_length
+        self.max_episode_length = cfg.max_episode_length or info.max_episode_length
         self.uses_actions = bool(info.uses_actions)
         self.dt = cfg.dt
 

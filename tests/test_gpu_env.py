@@ -274,3 +274,27 @@ def test_episode_stats_kernel(ouz, task, n):
     assert float(tot[1]) > 0, "no episode finished: the test would not test anything"
     torch.testing.assert_close(end, tot, rtol=1e-5, atol=1e-3)
     assert float(env.episode_stats()[1]) == 0.0          # drained
+
+
+def test_rlgames_creator_and_max_episode_override(ouz):
+    """A task YAML with maxEpisodeLength 30 (cfg/task/*.yaml) through the rl_games creator: the
+    time-outs fire where the oracle's do, at progress 29 (vec_task.py:348-351)."""
+    from ouzelum_amd import rlgames as R
+    cfg = R.resolve_task_config({"name": "LeeLanded", "env": {"numEnvs": "${resolve_default:4096,${...num_envs}}",
+                                                              "maxEpisodeLength": 30},
+                                 "sim": {"dt": 0.01, "substeps": 2}}, num_envs=256)
+    env = R.get_rlgames_env_creator(3, cfg, "LeeLanded", "cuda:0", "cuda:0", -1, True)()
+    assert env.num_envs == 256 and env.max_episode_length == 30
+    info = R.RLGPUEnv.__new__(R.RLGPUEnv)
+    info.env = env
+    assert info.get_env_info()["observation_space"].shape == (13,)
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_LEE_LANDED, num_envs=256, seed=3, max_episode_length=30))
+    saw = False
+    for k in range(62):
+        env.step(None)
+        o.step(np.zeros((256, 4)))
+        torch.cuda.synchronize()
+        to = env.timeout_buf.cpu().numpy()
+        np.testing.assert_array_equal(to, o.timeouts.astype(bool), err_msg=f"step {k}")
+        saw |= bool(to.any())
+    assert saw

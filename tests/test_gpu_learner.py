@@ -92,3 +92,7 @@ def test_training_loop_runs(tmp_path, algo, env, n):
     agent.load(str(tmp_path / "ck" / name))
     for k, v in agent.actor.state_dict().items():
         assert torch.equal(v, before[k])
+    # play mode on the saved policy (RPO-LSTM/play.py)
+    res = main(["--algo", algo, "--env", env, "--num_envs", str(n), "--total_steps", str(n * 20), "--play",
+                "--checkpoint", str(tmp_path / "ck" / name), "--quiet"])
+    assert np.isfinite(res["mean_reward"])
