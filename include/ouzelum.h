@@ -124,7 +124,8 @@ enum {
   OUZ_I_LAND_FLAG = 5,  /* self.flag                                            */
   OUZ_I_LANDINGS = 6,   /* per-env landing count (self.Landoa summed)           */
   OUZ_I_EP_CNT = 7,     /* episodes finished since last drain                   */
-  OUZ_I_COUNT = 8
+  OUZ_I_EP_LEN = 8,     /* summed lengths of those episodes (info["l"])          */
+  OUZ_I_COUNT = 9
 };
 
 typedef struct ouz_config {
@@ -186,13 +187,23 @@ int ouz_rollout(ouz_env* env, const float* action_ring, int32_t ring_len, int32_
                 float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, void* stream);
 int ouz_reset_idx(ouz_env* env, const int32_t* env_ids, int32_t n, void* stream);
 int ouz_reset_all(ouz_env* env, void* stream);
-/* Episode statistics of envs created with track_episodes: writes the f64 pair
- * out[0] = sum of returns, out[1] = count, of the episodes finished since the
- * last drain (device pointer, stream-ordered; one launch, deterministic order).
+/* Episode statistics of envs created with track_episodes: writes the f64 triple
+ * out[0] = sum of returns, out[1] = count, out[2] = sum of lengths, of the
+ * episodes finished since the last drain (device pointer, stream-ordered; one launch, deterministic order).
  * drain != 0 zeroes the accumulators.  Replaces RecordEpisodeStatisticsTorch's
  * per-step host bookkeeping (PPO/utils.py:20-35); the pair is what config E
- * all-reduces over RCCL. */
+ * all-reduces over RCCL (sum and count; the lengths give info["l"]). */
 int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream);
+
+/* Per-step trace of one env + per-step reset counts, written by the step kernel
+ * itself (no extra launch, no host sync).  Feeds the reference's trajectory CSV
+ * (ekf_lee_landed.py:132-135,667-674: env 0's position, target, velocity every
+ * step, one file per cumulative episode count) and metrics/<pomdp>_<prob>_ep_count.txt
+ * (:319-331).  Slot s % capacity of trace[capacity][9] holds (p, target, v) of
+ * env_index after step s; resets[s % capacity] = envs reset at the start of
+ * step s.  capacity >= 64 (the fused rollout runs waves up to 32 steps apart);
+ * capacity 0 disables.  The host must read slots before they are reused. */
+int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity);
 int64_t ouz_get_step(const ouz_env* env);
 int ouz_set_step(ouz_env* env, int64_t step);
 

@@ -34,8 +34,8 @@ F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
 F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
 F_EP_RET, F_EP_SUM = 101, 102
 F_COUNT = 103
-I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT = range(8)
-I_COUNT = 8
+I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT, I_EP_LEN = range(9)
+I_COUNT = 9
 TILE = 64  # OUZ_TILE: state is [tiles][fields][64] (ouzelum.h OUZ_FIDX)
 
 
@@ -89,6 +89,7 @@ SIGNATURES = {
     "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
     "ouz_reset_all": (_I, [_P, _P]),
     "ouz_episode_stats": (_I, [_P, _P, _I, _P]),
+    "ouz_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_get_step": (_I64, [_P]),
     "ouz_set_step": (_I, [_P, _I64]),
     "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),

@@ -81,6 +81,9 @@ struct StepArgs {
   uint64_t n_total;
   uint64_t seed;
   int32_t track_episodes;
+  float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
+  uint32_t* trace_resets;      // [trace_cap] envs reset at the start of each step
+  int32_t trace_env, trace_cap;
   EnvConsts c;
   TaskParams tp[OUZ_NUM_TASKS];
 };
@@ -211,7 +214,7 @@ struct EnvRegs {
   int32_t ttype, tidx;
   float sd;
   int32_t land_flag;              // -1: not loaded (only needed on reset / landing)
-  int32_t landings_add, ep_cnt_add;
+  int32_t landings_add, ep_cnt_add, ep_len_add;
   float ep_ret, ep_sum_add;
   uint32_t dirty;
 };
@@ -228,6 +231,7 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   S.land_flag = -1;
   S.landings_add = 0;
   S.ep_cnt_add = 0;
+  S.ep_len_add = 0;
   S.ep_sum_add = 0.0f;
   S.ep_ret = a.track_episodes ? ld(S.T, OUZ_F_EP_RET) : 0.0f;
   S.dr_m = S.dr_i = S.dr_t = 1.0f;
@@ -272,6 +276,7 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
     if (S.ep_cnt_add) {
       st(S.T, OUZ_F_EP_SUM, ld(S.T, OUZ_F_EP_SUM) + S.ep_sum_add);
       sti(S.T, OUZ_I_EP_CNT, ldi(S.T, OUZ_I_EP_CNT) + S.ep_cnt_add);
+      sti(S.T, OUZ_I_EP_LEN, ldi(S.T, OUZ_I_EP_LEN) + S.ep_len_add);
     }
   }
   if (S.landings_add) sti(S.T, OUZ_I_LANDINGS, ldi(S.T, OUZ_I_LANDINGS) + S.landings_add);
@@ -516,9 +521,15 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
   timeout = timeout_len && rs;                                             // vec_task.py:345
   if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
     S.ep_ret += rew;
-    if (rs) { S.ep_sum_add += S.ep_ret; S.ep_cnt_add += 1; S.ep_ret = 0.0f; }
+    if (rs) { S.ep_sum_add += S.ep_ret; S.ep_cnt_add += 1; S.ep_len_add += S.progress; S.ep_ret = 0.0f; }
   }
   S.rst = rs;
+  if (a.trace_cap > 0 && i == a.trace_env) {   // trajectory CSV row (ekf_lee_landed.py:667-674)
+    float* t = a.trace + (size_t)(sc.step % (uint32_t)a.trace_cap) * 9;
+    t[0] = p.x; t[1] = p.y; t[2] = p.z;
+    t[3] = target.x; t[4] = target.y; t[5] = target.z;
+    t[6] = v.x; t[7] = v.y; t[8] = v.z;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -580,6 +591,16 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
   wave_lds_sync();
 }
 
+// Per-step reset count for the trace (metrics/<pomdp>_<prob>_ep_count.txt, ekf_lee_landed.py:315-320):
+// one atomic per wave with resets; env 0 clears the slot 32 steps ahead (fused rollouts run waves
+// at most 31 steps apart, and the capacity is >= 64).
+__device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bool did_reset, int i) {
+  if (a.trace_cap <= 0) return;
+  const uint64_t m = __ballot(did_reset);
+  if ((i & 63) == 0 && m) atomicAdd(&a.trace_resets[step % (uint32_t)a.trace_cap], (uint32_t)__popcll(m));
+  if (i == 0) a.trace_resets[(step + 32u) % (uint32_t)a.trace_cap] = 0u;
+}
+
 // K steps of one env: load once, K x (step + emit), store once.  MULTI = false is the single
 // VecTask.step kernel (K = 1, no loop, no rollout storage) and keeps the register budget of one step.
 template <int CTRL, int TGT, bool MULTI>
@@ -598,7 +619,9 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
 #ifdef OUZ_PROBE_NOCORE
     for (int k = 0; k < OUZ_NUM_OBS; ++k) ob[k] = S.p.x * k;
 #else
+    const bool did_reset = valid && S.rst;
     if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
+    trace_count(a, ctx[0].step, did_reset, i);
 #endif
     emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
   } else {
@@ -606,7 +629,9 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       float ob[OUZ_NUM_OBS];
       float rew = 0.0f;
       bool rs = false, to = false;
+      const bool did_reset = valid && S.rst;
       if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
+      trace_count(a, ctx[k].step, did_reset, i);
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
         o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
@@ -721,42 +746,46 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-__global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, double2* partials, uint32_t* ticket,
+__global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, double* partials, uint32_t* ticket,
                                                                     double* out, int drain) {
-  __shared__ double s_sum[kStatsBlock / 64], s_cnt[kStatsBlock / 64];
+  __shared__ double s_part[3][kStatsBlock / 64];
   __shared__ bool s_last;
-  double sum = 0.0, cnt = 0.0;
+  double acc[3] = {0.0, 0.0, 0.0};   // sum of returns, count, sum of lengths
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
-    sum += (double)ld(a, OUZ_F_EP_SUM, i);
-    cnt += (double)ldi(a, OUZ_I_EP_CNT, i);
+    acc[0] += (double)ld(a, OUZ_F_EP_SUM, i);
+    acc[1] += (double)ldi(a, OUZ_I_EP_CNT, i);
+    acc[2] += (double)ldi(a, OUZ_I_EP_LEN, i);
     if (drain) {
       st(a, OUZ_F_EP_SUM, i, 0.0f);
       sti(a, OUZ_I_EP_CNT, i, 0);
+      sti(a, OUZ_I_EP_LEN, i, 0);
     }
   }
-  sum = wave_sum(sum);
-  cnt = wave_sum(cnt);
   const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { s_sum[w] = sum; s_cnt[w] = cnt; }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double v = wave_sum(acc[k]);
+    if ((threadIdx.x & 63) == 0) s_part[k][w] = v;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double2 p{0.0, 0.0};
-    for (int k = 0; k < kStatsBlock / 64; ++k) { p.x += s_sum[k]; p.y += s_cnt[k]; }
-    partials[blockIdx.x] = p;
+    for (int k = 0; k < 3; ++k) {
+      double p = 0.0;
+      for (int j = 0; j < kStatsBlock / 64; ++j) p += s_part[k][j];
+      partials[blockIdx.x * 3 + k] = p;
+    }
     __threadfence();
     s_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (s_last && threadIdx.x == 0) {
     __threadfence();
-    double2 t{0.0, 0.0};
-    for (unsigned b = 0; b < gridDim.x; ++b) {
-      const double2 p = partials[b];
-      t.x += p.x;
-      t.y += p.y;
-    }
-    out[0] = t.x;
-    out[1] = t.y;
+    double t[3] = {0.0, 0.0, 0.0};
+    for (unsigned b = 0; b < gridDim.x; ++b)
+      for (int k = 0; k < 3; ++k) t[k] += partials[b * 3 + k];
+    out[0] = t[0];
+    out[1] = t[1];
+    out[2] = t[2];
     *ticket = 0u;   // ready for the next launch on this stream
   }
 }
@@ -922,7 +951,7 @@ struct ouz_env {
   bool bound;
   int64_t step;
   float2* wp_tab;   // device waypoint tables
-  double2* stats_partials;   // [kStatsMaxBlocks] per-block partials of episode_stats_kernel
+  double* stats_partials;    // [kStatsMaxBlocks][3] per-block partials of episode_stats_kernel
   uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
 };
@@ -1002,10 +1031,10 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   if (r) { delete e; return r; }
   r = hip_check(hipMemcpy(e->wp_tab, host_tab, sizeof(host_tab), hipMemcpyHostToDevice), "hipMemcpy(waypoints)");
   if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
-  r = hip_check(hipMalloc(&e->stats_partials, kStatsMaxBlocks * sizeof(double2) + sizeof(uint32_t)),
+  r = hip_check(hipMalloc(&e->stats_partials, kStatsMaxBlocks * 3 * sizeof(double) + sizeof(uint32_t)),
                 "hipMalloc(stats)");
   if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
-  e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks);
+  e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
   r = hip_check(hipMemset(e->stats_ticket, 0, sizeof(uint32_t)), "hipMemset(stats)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   StepArgs& a = e->args;
@@ -1016,6 +1045,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   a.n_total = (uint64_t)total;
   a.seed = cfg->seed;
   a.track_episodes = cfg->track_episodes;
+  a.trace_env = -1;
   // x500 lumped mass properties (assets/x500/x500.urdf:31-35,98-177)
   const double base_m = 2.0, rm = 0.016076923076923075;
   const double mass = base_m + 4 * rm;
@@ -1213,6 +1243,25 @@ int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream) {
   hipLaunchKernelGGL(episode_stats_kernel, dim3(grid), dim3(kStatsBlock), 0, (hipStream_t)stream, env->args,
                      env->stats_partials, env->stats_ticket, out, drain ? 1 : 0);
   OUZ_LAUNCH_CHECK("episode_stats_kernel");
+  return OUZ_OK;
+}
+
+int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity) {
+  if (!env) return fail(OUZ_ERR_INVALID, "ouz_set_trace: null env");
+  if (capacity == 0) {
+    env->args.trace = nullptr;
+    env->args.trace_resets = nullptr;
+    env->args.trace_cap = 0;
+    env->args.trace_env = -1;
+    return OUZ_OK;
+  }
+  if (capacity < 64) return fail(OUZ_ERR_INVALID, "ouz_set_trace: capacity must be >= 64 (or 0 to disable)");
+  if (!trace || !resets) return fail(OUZ_ERR_INVALID, "ouz_set_trace: null buffer");
+  if (env_index < 0 || env_index >= env->cfg.num_envs) return fail(OUZ_ERR_INVALID, "ouz_set_trace: bad env_index");
+  env->args.trace = trace;
+  env->args.trace_resets = resets;
+  env->args.trace_env = env_index;
+  env->args.trace_cap = capacity;
   return OUZ_OK;
 }
 

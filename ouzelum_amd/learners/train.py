@@ -6,7 +6,8 @@ Same loop as the reference: T-step rollout with the LSTM carry reset on done, th
 actor acting on the clean observations and training on the learner-side POMDP ones
 (App. B item 10; ``--rollout_obs pomdp`` gives the RPO-LSTM_Critic variant), one
 PPO update per rollout, best/final checkpoints under the reference's file names.
-TensorBoard is not installed: scalars go to ``<logdir>/<run>.csv``.  Episode
+TensorBoard is not installed: the scalars of PPO/main.py:102-116 (average reward, episodic
+return / length) go to ``<logdir>/<run>.csv``.  Episode
 statistics are the env's in-kernel [sum, count] (``ouz_episode_stats``), all-reduced
 over RCCL when launched with torchrun (one process per GPU, env ids sharded).
 """
@@ -75,8 +76,8 @@ def train(args):
         os.makedirs(args.logdir, exist_ok=True)
         fh = open(os.path.join(args.logdir, name + ".csv"), "w", newline="")
         writer = csv.writer(fh)
-        writer.writerow(["global_step", "average_reward", "episodes", "episodic_return", "pg_loss", "v_loss",
-                         "approx_kl", "clipfrac", "env_steps_per_s"])
+        writer.writerow(["global_step", "average_reward", "episodes", "episodic_return", "episodic_length",
+                         "pg_loss", "v_loss", "approx_kl", "clipfrac", "env_steps_per_s"])
 
     global_step = 0
     max_reward = -float("inf")
@@ -111,11 +112,13 @@ def train(args):
         sps = N * world * T / (time.perf_counter() - t0)
         row = {"global_step": global_step, "average_reward": float(mean_rew), "episodes": int(ep[1]),
                "episodic_return": float(ep[0] / ep[1]) if float(ep[1]) > 0 else float("nan"),
+               "episodic_length": float(ep[2] / ep[1]) if float(ep[1]) > 0 else float("nan"),
                **{k: float(v) for k, v in stats.items()}, "env_steps_per_s": sps}
         history.append(row)
         if rank == 0:
             writer.writerow([row[k] for k in ("global_step", "average_reward", "episodes", "episodic_return",
-                                              "pg_loss", "v_loss", "approx_kl", "clipfrac", "env_steps_per_s")])
+                                              "episodic_length", "pg_loss", "v_loss", "approx_kl", "clipfrac",
+                                              "env_steps_per_s")])
             if not args.quiet:
                 print(f"Step: {global_step}, Average rewards {row['average_reward']:.4f}, "
                       f"{sps / 1e6:.2f} M env-steps/s", flush=True)

@@ -110,7 +110,7 @@ class QuadVecTask:
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
             self.timeout_buf = torch.empty(n, dtype=torch.bool, device=self.device)
             self._zero_actions = torch.zeros((n, L.NUM_ACT), dtype=torch.float32, device=self.device)
-            self._stats_buf = torch.zeros(2, dtype=torch.float64, device=self.device)
+            self._stats_buf = torch.zeros(3, dtype=torch.float64, device=self.device)
         self.states_buf = torch.zeros((n, 0), dtype=torch.float32, device=self.device)
         self.extras = {}
         self.obs_dict = {}
@@ -218,16 +218,43 @@ class QuadVecTask:
         return int(self.istate[:, L.I_LANDINGS].sum().item())
 
     def episode_stats(self, drain=True):
-        """(sum of returns, count) of episodes finished since the last drain, as a float64
-        device tensor [sum, count] — the quantity config E all-reduces over RCCL.  One kernel
+        """[sum of returns, count, sum of lengths] of episodes finished since the last drain, as a
+        float64 device tensor — the quantities RecordEpisodeStatisticsTorch reports as info["r"] /
+        info["l"] (PPO/utils.py:20-35); config E all-reduces it over RCCL.  One kernel
         (``ouz_episode_stats``).  The tensor is returned by reference and overwritten by the next
-        call, like ``rew_buf``; clone it to keep it.
-        Needs ``track_episodes=True`` (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35)."""
+        call, like ``rew_buf``; clone it to keep it.  Needs ``track_episodes=True``."""
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
         L.check(L.lib.ouz_episode_stats(self._env, L.ptr(self._stats_buf), 1 if drain else 0, self._stream()),
                 "ouz_episode_stats")
         return self._stats_buf
+
+    def enable_trace(self, env_index=0, capacity=4096):
+        """Record (p, target, v) of one env and the number of envs reset at every step, written by
+        the step kernel itself (``ouz_set_trace``).  Read with ``trace_since``; see outputs.py."""
+        if capacity == 0:
+            L.check(L.lib.ouz_set_trace(self._env, None, None, 0, 0), "ouz_set_trace")
+            self._trace = None
+            return
+        tr = torch.zeros((capacity, 9), dtype=torch.float32, device=self.device)
+        rs = torch.zeros(capacity, dtype=torch.int32, device=self.device)
+        L.check(L.lib.ouz_set_trace(self._env, L.ptr(tr), L.ptr(rs), int(env_index), int(capacity)), "ouz_set_trace")
+        self._trace = (tr, rs, self.sim_step_count)
+
+    def trace_since(self, step):
+        """(steps, rows (k, 9) float32 numpy, resets (k,) int64 numpy) for steps [step, now)."""
+        if getattr(self, "_trace", None) is None:
+            raise RuntimeError("call enable_trace() first")
+        tr, rs, start = self._trace
+        now = self.sim_step_count
+        step = max(step, start)
+        cap = tr.shape[0]
+        if now - step > cap:
+            raise RuntimeError(f"trace overrun: {now - step} steps since {step}, capacity {cap}")
+        torch.cuda.synchronize(self.device)
+        steps = np.arange(step, now)
+        idx = torch.as_tensor(steps % cap, device=self.device)
+        return steps, tr[idx].cpu().numpy(), rs[idx].cpu().numpy().astype(np.int64)
 
     def zero_actions(self):
         return torch.zeros((self.num_envs, self.num_actions), dtype=torch.float32, device=self.rl_device)

@@ -251,19 +251,23 @@ def test_fused_rollout_matches_single_steps(ouz, task):
 @pytest.mark.parametrize("task,n", [("Ouzelum", 1000), ("QuadFault", 70000), ("QuadMixed", 4096)])
 def test_episode_stats_kernel(ouz, task, n):
     """ouz_episode_stats (one launch) == RecordEpisodeStatisticsTorch bookkeeping done on the
-    step outputs (PPO/utils.py:20-35): returns accumulate per env, a done adds the episode's
-    return to the sum and bumps the count.  70000 envs > 256 blocks x 256 exercises the grid stride."""
+    step outputs (PPO/utils.py:20-35): returns and lengths accumulate per env, a done adds the
+    episode's return and length to the sums and bumps the count.  70000 envs > 256 blocks x 256 exercises the grid stride."""
     env = ouz.make(seed=4, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True)
     g = torch.Generator(device="cuda").manual_seed(5)
     ep_ret = torch.zeros(n, dtype=torch.float64, device="cuda")
-    tot = torch.zeros(2, dtype=torch.float64, device="cuda")
+    ep_len = torch.zeros(n, dtype=torch.float64, device="cuda")
+    tot = torch.zeros(3, dtype=torch.float64, device="cuda")
     for k in range(60):
         env.step(torch.rand((n, 4), device="cuda", generator=g) * 2 - 1)
         ep_ret += env.rew_buf.double()
+        ep_len += 1
         done = env.reset_buf.bool()
         tot[0] += ep_ret[done].sum()
         tot[1] += done.sum()
+        tot[2] += ep_len[done].sum()
         ep_ret[done] = 0
+        ep_len[done] = 0
         if k == 29:   # a non-draining peek, then a drain half way
             peek = env.episode_stats(drain=False).clone()
             mid = env.episode_stats().clone()
@@ -298,3 +302,58 @@ def test_rlgames_creator_and_max_episode_override(ouz):
         np.testing.assert_array_equal(to, o.timeouts.astype(bool), err_msg=f"step {k}")
         saw |= bool(to.any())
     assert saw
+
+
+def test_trace_trajectory_csv_and_metrics(ouz, tmp_path):
+    """The kernel-written trace reproduces the reference's per-step env-0 log (ekf_lee_landed.py:
+    667-674) and episode counter (:315-320): rows == (p, target, v) of env 0 after each step,
+    files split on the cumulative reset count; the fused rollout writes the same trace."""
+    from ouzelum_amd.outputs import TrajectoryLogger, load_env_state, save_env_state
+    import csv as _csv
+    n = 256
+    env = ouz.make(seed=5, task="EKFLeeLanded", num_envs=n, sim_device="cuda:0", convergence_time=10)
+    log = TrajectoryLogger(env, traj_dir=str(tmp_path / "traj"), metrics_dir=str(tmp_path / "metrics"),
+                           capacity=64)
+    expect, resets, prev_reset = [], [], torch.ones(n, dtype=torch.int64, device="cuda")
+    for k in range(90):
+        resets.append(int(prev_reset.sum()))
+        env.step(None)
+        tgt = env.target_root_positions[0]
+        rs = env.root_states[0]
+        expect.append(torch.cat([rs[0:3], tgt, rs[7:10]]).cpu().numpy())
+        prev_reset = env.reset_buf.clone()
+        if k % 30 == 29:
+            assert log.flush() == 30
+    epis = np.cumsum(resets)
+    assert log.epi == int(epis[-1]) and epis[0] == n            # step 0 resets every env
+    rows_by_file = {}
+    for e, row in zip(epis, expect):
+        rows_by_file.setdefault(int(e), []).append(row)
+    for e, rows in rows_by_file.items():
+        with open(tmp_path / "traj" / f"{log.tag}_ep_{e}.csv") as fh:
+            got = list(_csv.reader(fh))
+        assert got[0] == ["Position X", "Position Y", "Position Z"]
+        np.testing.assert_allclose(np.array(got[1:], float), np.array(rows), rtol=1e-6, atol=1e-6)
+    assert (tmp_path / "metrics" / f"{log.tag}_ep_count.txt").read_text() == str(int(epis[-1]))
+    assert (tmp_path / "metrics" / f"{log.tag}.txt").read_text() == str(env.landings())
+    # env-state checkpoint round trip through a file
+    save_env_state(env, str(tmp_path / "env.pt"))
+    twin = ouz.make(seed=5, task="EKFLeeLanded", num_envs=n, sim_device="cuda:0", convergence_time=10)
+    load_env_state(twin, str(tmp_path / "env.pt"))
+    env.step(None)
+    twin.step(None)
+    torch.cuda.synchronize()
+    assert torch.equal(env.fstate, twin.fstate) and torch.equal(env.obs_buf, twin.obs_buf)
+    # fused rollout: same trace as single steps
+    a = ouz.make(seed=6, task="EKFLeeLanded", num_envs=n, sim_device="cuda:0", convergence_time=10)
+    b = ouz.make(seed=6, task="EKFLeeLanded", num_envs=n, sim_device="cuda:0", convergence_time=10)
+    a.enable_trace(3, 64)
+    b.enable_trace(3, 64)
+    a.rollout(None, 40, fused=True)
+    for _ in range(40):
+        b.step(None)
+    sa, ra, ca = a.trace_since(0)
+    sb, rb, cb = b.trace_since(0)
+    np.testing.assert_array_equal(sa, sb)
+    np.testing.assert_array_equal(ca, cb)
+    np.testing.assert_allclose(ra, rb, rtol=1e-5, atol=1e-5)
