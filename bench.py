@@ -47,8 +47,8 @@ BYTES_PER_ENV_STEP = {
     "QuadFault": _CORE + 2 * 12 + 2 * 16 + 16 + 12,
     # + prev_v (12), EKF q + packed P (56), PV x + packed P (216), waypoint (12), each r/w
     "EKFLeeLanded": _CORE + 2 * (12 + 56 + 216 + 12),
-    # + DR scales (12 r), platform xy (8 r/w), trajectory type / index / scale (12 r, 4 w)
-    "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 16 + 12 + 4,
+    # + DR scales (12 r), platform xy + heading (12 r/w), trajectory type / index / scale (12 r, 4 w)
+    "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 24 + 12 + 4,
 }
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0

@@ -112,7 +112,8 @@ enum {
   OUZ_F_FAULT_ETA = 100,/* faulty-rotor efficiency (1)                          */
   OUZ_F_EP_RET = 101,   /* running episode return (RecordEpisodeStatisticsTorch) */
   OUZ_F_EP_SUM = 102,   /* sum of returns of episodes finished since last drain  */
-  OUZ_F_COUNT = 103
+  OUZ_F_PLAT_HEADING = 103, /* husky heading, rad (differential-drive platform)    */
+  OUZ_F_COUNT = 104
 };
 /* Int32 fields of istate. */
 enum {
@@ -140,7 +141,7 @@ typedef struct ouz_config {
   float dt;                 /* sim.dt (0.01)                                     */
   int32_t substeps;         /* sim.substeps (2)                                  */
   int32_t convergence_time; /* EKF tasks: steps of estimator warm-up (300)       */
-  float plat_speed;         /* trajectory platform speed, m/s                    */
+  float plat_speed;         /* max husky speed, m/s (15 rad/s x 0.165 m wheels)   */
   float dr_lo, dr_hi;       /* DR scale range                                    */
   float fault_eta_hi;       /* faulty rotor efficiency ~ U(0, fault_eta_hi)      */
   float thrust_max;         /* RL thrust clamp (2000 N, ouzelum.py:91)           */

@@ -417,14 +417,61 @@ def quat_mul_xyzw(a, b):
     return np.concatenate([v, w], -1)
 
 
-def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, wmax=MAX_ANGVEL):
+# Landing deck of the husky (build-defined contact): the drone's root rests at
+# z 0.375 on the deck (the reference's recorded landings, trajectories/flicker_0.01_ep_5.csv),
+# footprint = the disk inscribed in the 0.5709 m wide chassis (husky.urdf:61-69).
+DECK_Z_REST = 0.375
+DECK_RADIUS = 0.5709 / 2
+# husky differential drive (utils/controllers.py:15-43; gains from landing.py:361)
+WHEEL_BASE, WHEEL_RADIUS, MAX_WHEEL_SPEED = 0.54, 0.165, 15.0
+DRIVE_GAIN_LIN, DRIVE_GAIN_ANG, DRIVE_ANG_THRESH = 3.0, 1000.0, 0.005
+
+
+def map_to_pi(a):
+    """utils/controllers.py:5-13 (one wrap; inputs lie in (-3 pi, 3 pi))."""
+    a = np.where(a > math.pi, a - 2 * math.pi, a)
+    return np.where(a <= -math.pi, a + 2 * math.pi, a)
+
+
+def drive_command(cur, tgt, heading, gains=(DRIVE_GAIN_LIN, DRIVE_GAIN_ANG), max_wheel=MAX_WHEEL_SPEED):
+    """differential_drive (utils/controllers.py:15-43) -> saturated (linear, angular) velocity and the
+    wheel speeds (right, left, right, left) it returns."""
+    dx, dy = tgt[:, 0] - cur[:, 0], tgt[:, 1] - cur[:, 1]
+    dth = map_to_pi(np.arctan2(dy, dx) - map_to_pi(heading))
+    dth = np.where((dth < DRIVE_ANG_THRESH) & (dth > -DRIVE_ANG_THRESH), 0.0, dth)
+    lin = np.sqrt(dx ** 2 + dy ** 2) * gains[0]
+    ang = dth * gains[1]
+    left = (2 * lin + ang * WHEEL_BASE) / (2 * WHEEL_RADIUS)
+    right = (2 * lin - ang * WHEEL_BASE) / (2 * WHEEL_RADIUS)
+    mx = np.maximum(np.abs(left), np.abs(right))
+    sc = np.where(mx > max_wheel, max_wheel / np.maximum(mx, 1e-30), 1.0)
+    wheels = np.stack([right * sc, left * sc, right * sc, left * sc], -1)
+    return lin * sc, ang * sc, wheels
+
+
+def deck_contact(p, v, w, on, plat, plat_v):
+    """Inelastic sticking contact with the deck: a drone inside the footprint and below the rest
+    height is put on the deck, moves with the platform, and stops rotating."""
+    dxy = p[:, 0:2] - plat
+    hit = on & ((dxy ** 2).sum(-1) < DECK_RADIUS ** 2) & (p[:, 2] < DECK_Z_REST)
+    if hit.any():
+        p, v, w = p.copy(), v.copy(), w.copy()
+        p[hit, 2] = DECK_Z_REST
+        v[hit, 0:2] = plat_v[hit]
+        v[hit, 2] = np.maximum(v[hit, 2], 0.0)
+        w[hit] = 0.0
+    return p, v, w
+
+
+def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, wmax=MAX_ANGVEL, contact=None):
     """Semi-implicit Euler over ``substeps`` sub-steps on a lumped rigid body.
 
     f_b, tau_b: body-frame force (N) and torque (N m) at the COM (LOCAL_SPACE,
     ekf_lee_landed.py:525).  mass (N,), inertia (N,3) diagonal.  Velocities are
     world frame (Isaac root-state convention).  |w| is clamped to
     ``wmax`` (asset max_angular_velocity).  Orientation uses the exact
-    exponential map of the world-frame angular velocity.
+    exponential map of the world-frame angular velocity.  ``contact`` adds the landing
+    deck after each sub-step's position update (``deck_contact``).
     """
     h = dt / substeps
     g = np.array([0.0, 0.0, -GRAVITY], dtype=p.dtype)
@@ -439,6 +486,8 @@ def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, w
         scale = np.where(n > wmax, wmax / np.maximum(n, 1e-30), 1.0)
         w = w * scale[:, None]
         p = p + h * v
+        if contact is not None:          # (on mask, platform xy, platform velocity xy)
+            p, v, w = deck_contact(p, v, w, *contact)
         n = np.linalg.norm(w, axis=-1)
         th = 0.5 * h * n
         s = np.where(th < 1e-4, 0.5 * h * (1.0 - th * th / 6.0), np.sin(th) / np.maximum(n, 1e-30))
@@ -555,7 +604,7 @@ class EnvConfig:
     dt: float = DT
     substeps: int = SUBSTEPS
     convergence_time: int = 300  # cfg/task/EKFLeeLanded.yaml:18 (in sim steps, ekf_lee_landed.py:339)
-    plat_speed: float = 1.0      # build-defined kinematic platform speed (m/s)
+    plat_speed: float = MAX_WHEEL_SPEED * WHEEL_RADIUS   # max husky speed (m/s): 15 rad/s wheels
     dr_lo: float = 0.9
     dr_hi: float = 1.1
     fault_eta_hi: float = 0.5
@@ -609,6 +658,8 @@ class OracleEnv:
         self.pv_P = np.broadcast_to(np.eye(9, dtype=dtype) * PV_P0, (n, 9, 9)).copy()
         self.waypoint = f(3)
         self.plat = f(2)
+        self.plat_heading = f()
+        self.plat_v = f(2)            # per-step platform velocity (0 for the static platform)
         self.traj_type = np.zeros(n, np.int64)
         self.traj_sd = f()
         self.traj_idx = np.zeros(n, np.int64)
@@ -700,8 +751,10 @@ class OracleEnv:
         # ---- physics (vec_task.py:332-335 -> build-defined integrator) ----
         mass = MASS * self.dr[:, 0]
         inertia = INERTIA[None, :] * self.dr[:, 1:2]
+        deck_on = np.array([self.specs[tt].target_mode != TGT_GOAL for tt in self.task_ids])
         self.p, self.q, self.v, self.w = integrate(self.p, self.q, self.v, self.w, f_b, tau_b,
-                                                   mass.astype(dtype), inertia.astype(dtype), dt, cfg.substeps)
+                                                   mass.astype(dtype), inertia.astype(dtype), dt, cfg.substeps,
+                                                   contact=(deck_on, self.plat, self.plat_v))
 
         # ---- post_physics_step (ekf_lee_landed.py:620-685) ----
         self.progress += 1
@@ -866,7 +919,9 @@ class OracleEnv:
         return int(self.task_ids[np.nonzero(m)[0][0]])
 
     def _platform_step(self, m, t):
-        """Kinematic stand-in for the husky driving the landing.py:319-364 waypoint logic."""
+        """The husky following its waypoints (landing.py:319-364) as a kinematic differential-drive
+        unicycle: wheel speeds from differential_drive (utils/controllers.py:15-43, gains (3, 1000)),
+        saturated at 15 rad/s, integrated over dt (PhysX's skid-steer dynamics are not modelled)."""
         cfg = self.cfg
         wp = self._traj_point(self.traj_idx)
         d = np.sqrt(((wp - self.plat) ** 2).sum(-1))
@@ -876,8 +931,9 @@ class OracleEnv:
         if done.any():
             self._new_traj(done, t)
         wp = self._traj_point(self.traj_idx)
-        vec = wp - self.plat
-        d = np.sqrt((vec ** 2).sum(-1))
-        stepl = np.minimum(cfg.plat_speed * cfg.dt, d)
-        mv = np.where(d[:, None] > 0, vec / np.maximum(d, 1e-30)[:, None] * stepl[:, None], 0.0)
-        self.plat[m] = (self.plat + mv)[m]
+        lin, ang, _ = drive_command(self.plat, wp, self.plat_heading, max_wheel=cfg.plat_speed / WHEEL_RADIUS)
+        th = map_to_pi(self.plat_heading + ang * cfg.dt)
+        pv = np.stack([lin * np.cos(th), lin * np.sin(th)], 1)
+        self.plat_heading[m] = th[m]
+        self.plat_v[m] = pv[m]
+        self.plat[m] = (self.plat + pv * cfg.dt)[m]

@@ -32,8 +32,8 @@ MIXED_CHUNK = 64
 MIXED_TASKS = (TASK_LEE_LANDED, TASK_TRACKING, TASK_FAULT)
 F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
 F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
-F_EP_RET, F_EP_SUM = 101, 102
-F_COUNT = 103
+F_EP_RET, F_EP_SUM, F_PLAT_HEADING = 101, 102, 103
+F_COUNT = 104
 I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT, I_EP_LEN = range(9)
 I_COUNT = 9
 TILE = 64  # OUZ_TILE: state is [tiles][fields][64] (ouzelum.h OUZ_FIDX)

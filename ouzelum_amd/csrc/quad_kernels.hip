@@ -93,6 +93,14 @@ __device__ __constant__ float kRotorX[4] = {0.174f, -0.174f, 0.174f, -0.174f};
 __device__ __constant__ float kRotorY[4] = {-0.174f, 0.174f, 0.174f, -0.174f};
 __device__ __constant__ float kRotorDir[4] = {1.0f, 1.0f, -1.0f, -1.0f};   // ccw ccw cw cw (model.sdf:516-575)
 constexpr float kMotorKm = 0.016f;
+// husky differential drive (utils/controllers.py:15-43; gains landing.py:361)
+constexpr float kWheelBase = 0.54f, kWheelRadius = 0.165f;
+constexpr float kDriveGainLin = 3.0f, kDriveGainAng = 1000.0f, kDriveAngThresh = 0.005f;
+constexpr float kPiF32 = 3.14159265358979f;
+__device__ __forceinline__ float map_to_pi(float a) {   // utils/controllers.py:5-13 (one wrap)
+  a = a > kPiF32 ? a - 2.0f * kPiF32 : a;
+  return a <= -kPiF32 ? a + 2.0f * kPiF32 : a;
+}
 constexpr int kTrajLen[3] = {100, 100, 4};
 constexpr int kTrajBase[3] = {0, 100, 200};
 
@@ -210,7 +218,9 @@ struct EnvRegs {
   V3 prev_v, wp;                  // CTRL_LEE_EST
   EkfQ eq;
   float eP[10], px[9], pP[45];
-  float2 plat;                    // TGT_TRAJ
+  float2 plat;                    // platform xy (TGT_TRAJ state; (0, 0) for TGT_PLATFORM)
+  float plat_th;                  // TGT_TRAJ: husky heading
+  float2 plat_v;                  // this step's platform velocity (deck contact)
   int32_t ttype, tidx;
   float sd;
   int32_t land_flag;              // -1: not loaded (only needed on reset / landing)
@@ -256,12 +266,15 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   }
   if constexpr (TGT == TGT_TRAJ) {
     S.plat = make_float2(ld(S.T, OUZ_F_PLAT), ld(S.T, OUZ_F_PLAT + 1));
+    S.plat_th = ld(S.T, OUZ_F_PLAT_HEADING);
     S.ttype = ldi(S.T, OUZ_I_TRAJ_TYPE);
     S.tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
     S.sd = ld(S.T, OUZ_F_TRAJ_SD);
   } else {
     S.plat = make_float2(0.0f, 0.0f);
+    S.plat_th = 0.0f;
   }
+  S.plat_v = make_float2(0.0f, 0.0f);
 }
 
 template <int CTRL, int TGT>
@@ -300,7 +313,7 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
     for (int k = 0; k < 45; ++k) st(S.T, OUZ_F_PV_P + k, S.pP[k]);
   }
   if constexpr (TGT == TGT_TRAJ) {
-    st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y);
+    st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y); st(S.T, OUZ_F_PLAT_HEADING, S.plat_th);
     sti(S.T, OUZ_I_TRAJ_IDX, S.tidx);
     if (S.dirty & D_TRAJ) { sti(S.T, OUZ_I_TRAJ_TYPE, S.ttype); st(S.T, OUZ_F_TRAJ_SD, S.sd); }
   }
@@ -415,13 +428,22 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
         S.tidx = 0;
         S.dirty |= D_TRAJ;
       }
+      // differential_drive (utils/controllers.py:15-43, gains (3, 1000) landing.py:361) on a
+      // kinematic unicycle; wheel speeds saturate at plat_speed / wheel radius (15 rad/s)
       wpp = traj_point(a, S.ttype, S.tidx, S.sd);
       dx = wpp.x - S.plat.x; dy = wpp.y - S.plat.y;
-      float d = sqrtf(dx * dx + dy * dy);
-      if (d > 0.0f) {
-        float s = fminf(c.plat_speed * c.dt, d) / d;
-        S.plat.x += dx * s; S.plat.y += dy * s;
-      }
+      float dth = map_to_pi(atan2f(dy, dx) - map_to_pi(S.plat_th));
+      if (fabsf(dth) < kDriveAngThresh) dth = 0.0f;
+      float lin = sqrtf(dx * dx + dy * dy) * kDriveGainLin, ang = dth * kDriveGainAng;
+      const float wl = (2.0f * lin + ang * kWheelBase) / (2.0f * kWheelRadius);
+      const float wr = (2.0f * lin - ang * kWheelBase) / (2.0f * kWheelRadius);
+      const float mx = fmaxf(fabsf(wl), fabsf(wr)), max_w = c.plat_speed / kWheelRadius;
+      if (mx > max_w) { const float sc = max_w / mx; lin *= sc; ang *= sc; }
+      S.plat_th = map_to_pi(S.plat_th + ang * c.dt);
+      float sn, cs;
+      sincosf(S.plat_th, &sn, &cs);
+      S.plat_v = make_float2(lin * cs, lin * sn);
+      S.plat.x += S.plat_v.x * c.dt; S.plat.y += S.plat_v.y * c.dt;
     }
     V3 lin_acc = v3((S.v.x - S.prev_v.x) / c.dt, (S.v.y - S.prev_v.y) / c.dt, (S.v.z - S.prev_v.z) / c.dt);
     lin_acc.z += 9.8f;                                 // aliasing quirk (ekf_lee_landed.py:366-367)
@@ -492,7 +514,8 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
-    integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax);
+    integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
+              DeckContact{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y});
   }
 
   // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
@@ -970,7 +993,7 @@ void ouz_default_config(ouz_config* c) {
   c->dt = 0.01f;
   c->substeps = 2;
   c->convergence_time = 300;
-  c->plat_speed = 1.0f;
+  c->plat_speed = 15.0f * 0.165f;   // max husky speed: 15 rad/s wheels (utils/controllers.py:22-24)
   c->dr_lo = 0.9f;
   c->dr_hi = 1.1f;
   c->fault_eta_hi = 0.5f;

@@ -578,8 +578,19 @@ constexpr float kGravity = 9.81f;
 
 // f_b / tau_b: body-frame force and torque at the COM (LOCAL_SPACE, ekf_lee_landed.py:525);
 // inv_I = 1/I (diagonal).  Semi-implicit Euler; exact exponential map for the attitude.
+// Landing deck of the husky (build-defined contact; oracle deck_contact): the drone
+// root rests at z 0.375 (the reference's recorded landings), footprint = the disk inscribed in the
+// 0.5709 m wide chassis (husky.urdf:61-69).  Inelastic, sticking: on the deck the drone moves with
+// the platform and stops rotating.
+constexpr float kDeckZRest = 0.375f;
+constexpr float kDeckRadius2 = (0.5709f * 0.5f) * (0.5709f * 0.5f);
+struct DeckContact {
+  bool on;
+  float px, py, vx, vy;   // platform position / velocity (xy)
+};
+
 OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m, V3 I, V3 inv_I, float dt,
-                      int substeps, float wmax) {
+                      int substeps, float wmax, DeckContact deck = DeckContact{false, 0.f, 0.f, 0.f, 0.f}) {
   const float h = dt / (float)substeps;
   for (int s = 0; s < substeps; ++s) {
     M3 R = quat_to_mat(q);
@@ -592,6 +603,14 @@ OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m,
     float n2 = dot(w, w);
     if (n2 > wmax * wmax) w = (wmax / sqrtf(n2)) * w;
     p = p + h * v;
+    if (deck.on) {
+      const float dx = p.x - deck.px, dy = p.y - deck.py;
+      if (dx * dx + dy * dy < kDeckRadius2 && p.z < kDeckZRest) {
+        p.z = kDeckZRest;
+        v = v3(deck.vx, deck.vy, fmaxf(v.z, 0.0f));
+        w = v3(0.0f, 0.0f, 0.0f);
+      }
+    }
     // dq = [sin(th) w/|w|, cos(th)], th = |w| h / 2.  |w| <= wmax keeps th small at the
     // configured dt (4 pi * 0.005 / 2 = 0.031 rad): there the Taylor series to th^5 / th^6
     // is exact in f32 and replaces the libm sin/cos.

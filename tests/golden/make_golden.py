@@ -21,6 +21,8 @@ and writes small ``.npz`` fixtures next to itself.  The fixtures are data
 * Trajectories  isaacgymenvs/utils/trajectories.py.
 * Quaternion rotate (xyzw)  isaacgymenvs/tasks/amp/poselib/poselib/core/rotation3d.py
   (quat_rotate) — the importable twin of isaacgym.torch_utils.quat_rotate.
+* Husky drive  isaacgymenvs/utils/controllers.py::differential_drive (wheel speeds for random
+  poses / targets / headings, landing.py's gains and the defaults).
 * Learner  isaacgymenvs/RPO-LSTM/{model,agent}.py — ``PPO.getGAE`` run unbound on a
   stub ``self`` (critic = fixed next values), and the LSTM actor's ``get_states`` /
   ``actor_mean`` / critic forward with the module's own seeded initialisation
@@ -248,6 +250,21 @@ def gen_traj_and_quat(ref):
     np.savez_compressed(os.path.join(HERE, "traj_quat.npz"), **out)
 
 
+def gen_drive(ref):
+    """utils/controllers.py::differential_drive with landing.py:361's gains (3, 1000)."""
+    ctl = _load("ref_controllers", os.path.join(ref, "isaacgymenvs", "utils", "controllers.py"))
+    rs = np.random.RandomState(6000)
+    n = 200
+    cur = rs.uniform(-4, 4, (n, 2))
+    tgt = cur + rs.normal(0, 1.0, (n, 2)) * rs.choice([0.01, 0.3, 3.0], (n, 1))
+    head = rs.uniform(-np.pi, np.pi, n)
+    head[:10] = np.arctan2(tgt[:10, 1] - cur[:10, 1], tgt[:10, 0] - cur[:10, 0])   # aligned: dtheta below threshold
+    out = {"cur": cur, "tgt": tgt, "heading": head}
+    for g, name in (((3.0, 1000.0), "wheels_landing"), ((0.5, 10.0), "wheels_default")):
+        out[name] = ctl.differential_drive(torch.tensor(cur), torch.tensor(tgt), torch.tensor(head), g).numpy()
+    np.savez_compressed(os.path.join(HERE, "drive.npz"), **out)
+
+
 def gen_learner(ref):
     d = os.path.join(ref, "isaacgymenvs", "RPO-LSTM")
     model = _load("model", os.path.join(d, "model.py"))      # agent.py does `from model import ...`
@@ -302,4 +319,5 @@ if __name__ == "__main__":
     gen_pv(a.ref)
     gen_traj_and_quat(a.ref)
     gen_learner(a.ref)
+    gen_drive(a.ref)
     print("golden fixtures written to", HERE)

@@ -58,6 +58,7 @@ def gpu_to_oracle(env, oenv):
     oenv.pv_P = unpack_sym(f[L.F_PV_P:L.F_PV_P + 45].T.copy(), 9)
     oenv.waypoint = f[L.F_WAYPOINT:L.F_WAYPOINT + 3].T.copy()
     oenv.plat = f[L.F_PLAT:L.F_PLAT + 2].T.copy()
+    oenv.plat_heading = f[L.F_PLAT_HEADING].copy()
     oenv.traj_sd = f[L.F_TRAJ_SD].copy()
     oenv.dr = f[L.F_DR:L.F_DR + 3].T.copy()
     oenv.fault_eta = f[L.F_FAULT_ETA].copy()

@@ -93,6 +93,37 @@ def test_single_step_parity(ouz, task):
             env.step(torch.as_tensor(a, device="cuda"))
 
 
+@pytest.mark.parametrize("task", ["EKFLeeLanded", "QuadTracking", "LeeLanded"])
+def test_single_step_parity_on_the_deck(ouz, task):
+    """Single-step parity late in the episode, when most drones sit on the landing deck (build-defined
+    contact) and the QuadTracking platform drives its differential-drive path."""
+    from ouzelum_amd import _lib as L
+    n = 320
+    env, o = make_pair(ouz, task, n, seed=17, convergence_time=30)
+    for _ in range(260):
+        env.step(None)
+    for k in range(3):
+        gpu_to_oracle(env, o)
+        o.step(np.zeros((n, 4)))
+        env.step(None)
+        g, r = gpu_snapshot(env), oracle_snapshot(o)
+        ok = ~near_threshold(o)
+        on_deck = np.abs(r["p"][:, 2] - Q.DECK_Z_REST) < 1e-9
+        if task != "LeeLanded":
+            assert on_deck.sum() > n // 4, f"only {on_deck.sum()} drones on the deck"
+        assert_close(f"{task} deck p", g["p"][ok], r["p"][ok], 2e-5, 2e-5)
+        assert_close(f"{task} deck v", g["v"][ok], r["v"][ok], 1e-4, 1e-5)
+        assert_close(f"{task} deck w", g["w"][ok], r["w"][ok], 1e-3, 1e-4)
+        assert_close(f"{task} deck obs", g["obs"][ok], r["obs"][ok], 1e-4, 1e-5)
+        assert_close(f"{task} deck rew", g["rew"][ok], r["rew"][ok], 1e-5, 1e-5)
+        np.testing.assert_array_equal(g["reset"][ok], r["reset"][ok])
+        if task == "QuadTracking":
+            assert_close(f"{task} plat", g["plat"], r["plat"], 1e-5, 1e-6)
+            head = env.frows(L.F_PLAT_HEADING)[0].cpu().numpy()
+            dh = np.angle(np.exp(1j * (head - o.plat_heading)))
+            assert np.abs(dh).max() < 1e-4
+
+
 @pytest.mark.parametrize("task", ["LeeLanded", "EKFLeeLanded", "QuadTracking"])
 def test_free_run_closed_loop(ouz, task):
     """Closed-loop Lee tasks are contractive: free-running f32 GPU and f64 oracle stay close."""

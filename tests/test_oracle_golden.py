@@ -87,3 +87,35 @@ def test_reference_f32_pvfilter_is_ill_conditioned(golden):
         x, x32 = g[f"s{seed}_x"], g[f"s{seed}_x_f32ref"].astype(np.float64)
         rel = np.abs(x32 - x).max(-1) / np.maximum(1.0, np.abs(x).max(-1))
         assert rel.max() > 0.1
+
+
+def test_differential_drive_matches_reference(golden):
+    """Husky wheel speeds (utils/controllers.py:15-43) for landing.py's gains and the defaults."""
+    g = golden("drive.npz")
+    for gains, key in (((3.0, 1000.0), "wheels_landing"), ((0.5, 10.0), "wheels_default")):
+        _, _, wheels = Q.drive_command(g["cur"], g["tgt"], g["heading"], gains)
+        np.testing.assert_allclose(wheels, g[key], rtol=1e-12, atol=1e-9)
+
+
+def test_deck_contact_and_platform_motion():
+    """Build-defined landing deck: a drone dropped inside the footprint comes to rest at z 0.375 and
+    rides the platform; outside it falls through; the trajectory platform follows its waypoints."""
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_EKF_LEE_LANDED, num_envs=2, seed=0, convergence_time=0))
+    o.step(np.zeros((2, 4)))
+    o.p[:] = [[0.05, 0.0, 0.6], [0.6, 0.0, 0.6]]     # inside / outside the deck disk (r 0.285)
+    o.v[:] = 0
+    o.w[:] = 0
+    p, q, v, w = o.p, o.q, o.v, o.w
+    on = np.array([True, True])
+    plat = np.zeros((2, 2))
+    pv = np.array([[0.3, 0.0], [0.3, 0.0]])
+    for _ in range(60):
+        p, q, v, w = Q.integrate(p, q, v, w, np.zeros((2, 3)), np.zeros((2, 3)), np.full(2, Q.MASS),
+                                 np.tile(Q.INERTIA, (2, 1)), contact=(on, plat, pv))
+    assert p[0, 2] == Q.DECK_Z_REST and v[0, 0] == 0.3 and np.all(w[0] == 0)
+    assert p[1, 2] < 0.3                                 # fell past the deck
+    tr = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_TRACKING, num_envs=8, seed=3, convergence_time=0))
+    for _ in range(300):
+        tr.step(np.zeros((8, 4)))
+    assert np.all(tr.traj_idx + (tr.traj_type * 0) >= 0) and np.abs(tr.plat).max() > 0.5
+    assert np.abs(np.sqrt((tr.plat_v ** 2).sum(-1))).max() <= Q.MAX_WHEEL_SPEED * Q.WHEEL_RADIUS + 1e-9
