@@ -14,12 +14,47 @@ Differences, all MI355X-side:
 * Minibatch permutations come from ``torch.randperm`` on the device (no H2D copy of
   a numpy permutation) and the clip fractions stay on the device until the end of
   the update (the reference syncs with ``.item()`` every minibatch).
+* Under torchrun (one process per GPU, env ids sharded) the learner is data
+  parallel: rank 0's initial weights are broadcast and every optimizer step
+  all-reduces one flattened gradient bucket over RCCL.  The reference learners are
+  single-GPU.
 """
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from .. import _lib as L
 from .models import Critic, LSTMActor, MLPActor
+
+
+def broadcast_params(module, src=0):
+    """Same initial weights on every rank (one flattened broadcast)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    flat = torch.cat([p.data.reshape(-1) for p in module.parameters()])
+    dist.broadcast(flat, src)
+    off = 0
+    for p in module.parameters():
+        n = p.numel()
+        p.data.copy_(flat[off:off + n].view_as(p))
+        off += n
+
+
+def allreduce_grads(module):
+    """Data-parallel gradient mean over ranks: ONE all-reduce of the flattened gradients per
+    optimizer step (the networks are < 1 M parameters, so a single bucket beats per-tensor calls
+    on xGMI's per-link ring)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    params = [p for p in module.parameters() if p.grad is not None]
+    flat = torch.cat([p.grad.reshape(-1) for p in params])
+    dist.all_reduce(flat)
+    flat /= dist.get_world_size()
+    off = 0
+    for p in params:
+        n = p.numel()
+        p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        off += n
 
 
 def gae(rewards, values, dones, next_value, next_done, gamma=0.99, lam=0.95):
@@ -63,6 +98,8 @@ class PPOLearner:
         self.actor = (LSTMActor(observation_space, action_space) if recurrent
                       else MLPActor(observation_space, action_space)).to(self.device)
         self.critic = Critic(observation_space).to(self.device)
+        broadcast_params(self.actor)
+        broadcast_params(self.critic)
         self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr, eps=1e-5)
         self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=lr, eps=1e-5)
 
@@ -134,11 +171,13 @@ class PPOLearner:
 
                 self.actor_optimizer.zero_grad()
                 actor_loss.backward()
+                allreduce_grads(self.actor)            # data parallel over ranks (no-op on one GPU)
                 nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad_norm)
                 self.actor_optimizer.step()
 
                 self.critic_optimizer.zero_grad()
                 critic_loss.backward()
+                allreduce_grads(self.critic)
                 nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad_norm)
                 self.critic_optimizer.step()
                 stats = {"pg_loss": pg_loss.detach(), "v_loss": v_loss.detach(), "approx_kl": approx_kl}

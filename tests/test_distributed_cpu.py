@@ -88,3 +88,44 @@ def test_shard_ranges():
     from ouzelum_amd.distributed import shard
     assert shard(4096, 0, 8) == (0, 32768)
     assert shard(4096, 7, 8) == (7 * 4096, 32768)
+
+
+def _grad_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from ouzelum_amd.distributed import init_from_env
+    from ouzelum_amd.learners.models import Critic
+    from ouzelum_amd.learners.ppo import allreduce_grads, broadcast_params
+    from ouzelum_amd.spaces import Box
+    init_from_env(backend="gloo")
+    torch.manual_seed(100 + rank)                    # different init per rank ...
+    net = Critic(Box(-np.inf * np.ones(13), np.inf * np.ones(13)))
+    broadcast_params(net)                            # ... made identical
+    x = torch.randn(32, 13, generator=torch.Generator().manual_seed(rank))
+    net(x).pow(2).mean().backward()
+    allreduce_grads(net)
+    torch.save({k: v.clone() for k, v in net.state_dict().items()}, os.path.join(out_dir, f"w{rank}.pt"))
+    torch.save([p.grad.clone() for p in net.parameters()], os.path.join(out_dir, f"g{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_learner_data_parallel_gradients(tmp_path):
+    """broadcast_params + allreduce_grads == one learner on the union of both ranks' minibatches."""
+    from ouzelum_amd.learners.models import Critic
+    from ouzelum_amd.spaces import Box
+    mp.spawn(_grad_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    w0 = torch.load(tmp_path / "w0.pt", weights_only=True)
+    w1 = torch.load(tmp_path / "w1.pt", weights_only=True)
+    for k in w0:
+        assert torch.equal(w0[k], w1[k])
+    g0 = torch.load(tmp_path / "g0.pt", weights_only=True)
+    g1 = torch.load(tmp_path / "g1.pt", weights_only=True)
+    net = Critic(Box(-np.inf * np.ones(13), np.inf * np.ones(13)))
+    net.load_state_dict(w0)
+    xs = [torch.randn(32, 13, generator=torch.Generator().manual_seed(r)) for r in range(2)]
+    loss = sum(net(x).pow(2).mean() for x in xs) / 2
+    loss.backward()
+    for a, b, p in zip(g0, g1, net.parameters()):
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a, p.grad, rtol=1e-5, atol=1e-7)
