@@ -245,6 +245,20 @@ int ouz_gae(const float* rewards, const float* values, const float* dones, const
 int ouz_pomdp_obs(const float* in, float* out, int32_t rows, int32_t dim, int32_t mode, float prob, uint64_t seed,
                   int64_t row_offset, uint32_t call, void* stream);
 
+/* Fused LSTM cell for the recurrent actor (RPO-LSTM/model.py:27-50; torch gate order
+ * i, f, g, o).  gates [B][4H] = x W_ih^T + b + (keep * h) W_hh^T, pre-activation;
+ * c_prev_m [B][H] the masked carry; keep_next [B] (1 - done of the next step, or
+ * null = 1).  Writes the activated gates act [B][4H] (saved for BPTT), c_out, h_out
+ * and the next step's masked carry h_next_m / c_next_m. */
+int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* keep_next, float* act, float* c_out,
+                      float* h_out, float* h_next_m, float* c_next_m, int32_t B, int32_t H, void* stream);
+/* BPTT of one step: dh = dhid + keep_next * G (G = dgates_{t+1} W_hh, or null),
+ * dc = keep_next * dc_next (or null) + dh o (1 - tanh(c)^2); writes dgates [B][4H]
+ * (pre-activation) and dc_prev [B][H] (gradient of the masked carry). */
+int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, const float* dhid, const float* G,
+                      const float* dc_next, const float* keep_next, float* dgates, float* dc_prev, int32_t B, int32_t H,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

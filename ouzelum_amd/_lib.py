@@ -102,6 +102,8 @@ SIGNATURES = {
     "ouz_philox": (_I, [_U64, _P, _U32, _U32, _U32, _P, _I, _P]),
     "ouz_gae": (_I, [_P, _P, _P, _P, _P, _I, _I, _F, _F, _P, _P, _P]),
     "ouz_pomdp_obs": (_I, [_P, _P, _I, _I, _I, _F, _U64, _I64, _U32, _P]),
+    "ouz_lstm_cell_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "ouz_lstm_cell_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
 }
 
 

@@ -71,6 +71,62 @@ __global__ void __launch_bounds__(256) pomdp_obs_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused LSTM cell (RPO-LSTM/model.py:27-50, torch's gate order i, f, g, o).  The recurrent
+// GEMM gates = x W_ih^T + b + h W_hh^T stays in hipBLASLt; everything element-wise around it —
+// 4 activations, the cell update, tanh(c), the done-mask of the NEXT step's carry and the
+// saved activations for BPTT — is one launch per step instead of ~10 torch kernels.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ void __launch_bounds__(256) lstm_cell_fwd_kernel(const float* __restrict__ gates,
+                                                            const float* __restrict__ c_prev_m,
+                                                            const float* __restrict__ keep_next,
+                                                            float* __restrict__ act, float* __restrict__ c_out,
+                                                            float* __restrict__ h_out, float* __restrict__ h_next_m,
+                                                            float* __restrict__ c_next_m, int B, int H) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H) return;
+  const int b = idx / H, j = idx - b * H;
+  const float* g = gates + (size_t)b * 4 * H;
+  const float ig = sigm(g[j]), fg = sigm(g[H + j]), gg = tanhf(g[2 * H + j]), og = sigm(g[3 * H + j]);
+  const float c = fg * c_prev_m[idx] + ig * gg;
+  const float h = og * tanhf(c);
+  float* a = act + (size_t)b * 4 * H;
+  a[j] = ig; a[H + j] = fg; a[2 * H + j] = gg; a[3 * H + j] = og;
+  c_out[idx] = c;
+  h_out[idx] = h;
+  const float k = keep_next ? keep_next[b] : 1.0f;
+  h_next_m[idx] = k * h;
+  c_next_m[idx] = k * c;
+}
+
+// BPTT for one step.  dh = dhid + keep_next * G (G = dgates_{t+1} W_hh, null at the last step),
+// dc = dc_next * keep_next (dc_next = the next step's d c_prev, or the loss's dcT at the last step).
+__global__ void __launch_bounds__(256) lstm_cell_bwd_kernel(const float* __restrict__ act, const float* __restrict__ c,
+                                                            const float* __restrict__ c_prev_m,
+                                                            const float* __restrict__ dhid, const float* __restrict__ G,
+                                                            const float* __restrict__ dc_next,
+                                                            const float* __restrict__ keep_next,
+                                                            float* __restrict__ dgates, float* __restrict__ dc_prev,
+                                                            int B, int H) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * H) return;
+  const int b = idx / H, j = idx - b * H;
+  const float k = keep_next ? keep_next[b] : 1.0f;
+  const float dh = dhid[idx] + (G ? k * G[idx] : 0.0f);
+  const float* a = act + (size_t)b * 4 * H;
+  const float ig = a[j], fg = a[H + j], gg = a[2 * H + j], og = a[3 * H + j];
+  const float tc = tanhf(c[idx]);
+  const float dc = (dc_next ? k * dc_next[idx] : 0.0f) + dh * og * (1.0f - tc * tc);
+  float* d = dgates + (size_t)b * 4 * H;
+  d[j] = dc * gg * ig * (1.0f - ig);
+  d[H + j] = dc * c_prev_m[idx] * fg * (1.0f - fg);
+  d[2 * H + j] = dc * ig * (1.0f - gg * gg);
+  d[3 * H + j] = dh * tc * og * (1.0f - og);
+  dc_prev[idx] = dc * fg;
+}
+
 inline int grid(int n, int b) { return (n + b - 1) / b; }
 
 int launch_status(const char* what) {
@@ -119,6 +175,27 @@ int ouz_pomdp_obs(const float* in, float* out, int32_t rows, int32_t dim, int32_
   hipLaunchKernelGGL(pomdp_obs_kernel, dim3(grid(rows, 256)), dim3(256), 0, (hipStream_t)stream, in, out, rows, dim,
                      zero, noise, lo, hi, seed, (uint32_t)row_offset, call);
   return launch_status("pomdp_obs_kernel");
+}
+
+int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* keep_next, float* act, float* c_out,
+                      float* h_out, float* h_next_m, float* c_next_m, int32_t B, int32_t H, void* stream) {
+  if (B <= 0 || H <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_cell_fwd: B and H must be > 0");
+  if (!gates || !c_prev_m || !act || !c_out || !h_out || !h_next_m || !c_next_m)
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_cell_fwd: null buffer");
+  hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(grid(B * H, 256)), dim3(256), 0, (hipStream_t)stream, gates, c_prev_m,
+                     keep_next, act, c_out, h_out, h_next_m, c_next_m, B, H);
+  return launch_status("lstm_cell_fwd_kernel");
+}
+
+int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, const float* dhid, const float* G,
+                      const float* dc_next, const float* keep_next, float* dgates, float* dc_prev, int32_t B, int32_t H,
+                      void* stream) {
+  if (B <= 0 || H <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_cell_bwd: B and H must be > 0");
+  if (!act || !c || !c_prev_m || !dhid || !dgates || !dc_prev)
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_cell_bwd: null buffer");
+  hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(grid(B * H, 256)), dim3(256), 0, (hipStream_t)stream, act, c, c_prev_m,
+                     dhid, G, dc_next, keep_next, dgates, dc_prev, B, H);
+  return launch_status("lstm_cell_bwd_kernel");
 }
 
 }  // extern "C"

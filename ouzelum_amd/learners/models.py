@@ -7,9 +7,11 @@ load unchanged), with the recurrent actor restructured for the GPU:
 * ``LSTMActor.get_states`` (reference ``model.py:34-50``) calls ``nn.LSTM`` once
   per time step because the done mask resets the carry between steps.  Here the
   input projection ``x W_ihᵀ + b_ih + b_hh`` of all T steps is one GEMM over
-  (T·B, 256) — hipBLASLt at a useful size — and only the (B,128)x(128,512)
-  recurrent product plus the gate nonlinearities remain per step.  Gate order
-  and arithmetic are torch's LSTM cell (i, f, g, o).
+  (T·B, 256) — hipBLASLt at a useful size — and on the GPU each step is one
+  (B,128)x(128,512) recurrent GEMM plus ONE fused HIP cell kernel, with a matching
+  fused BPTT (``fused.LSTMSequence``).  Gate order and arithmetic are torch's LSTM
+  cell (i, f, g, o); on CPU tensors the same math runs as torch ops.
+* Large-row linear layers take a split-K weight gradient (``fused.SplitKLinear``).
 * RPO's policy-update noise ``z ~ U(-alpha, alpha)`` (``model.py:61-64``) is drawn
   on the actor's device instead of a CPU ``FloatTensor`` copied to ``cuda:0``.
 """
@@ -19,6 +21,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 from torch.distributions.normal import Normal
+
+from .fused import LSTMSequence, SplitKLinear, run_mlp
 
 
 def layer_init(layer, std=math.sqrt(2), bias_const=0.0):
@@ -47,7 +51,7 @@ class MLPActor(nn.Module):
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
 
     def forward(self, state, action=None):
-        mean = self.actor_mean(state)
+        mean = run_mlp(self.actor_mean, state)
         return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha)
 
 
@@ -79,11 +83,19 @@ class LSTMActor(nn.Module):
     def get_states(self, state, lstm_state, done):
         """(T·B, obs) trunk features -> (T·B, H) LSTM outputs; the carry of env b is zeroed
         before step t when done[t, b] (model.py:34-50).  Returns (hidden, (h, c))."""
-        feats = self.network(state)
+        feats = run_mlp(self.network, state)
         h, c = lstm_state
         B = h.shape[1]
         H = self.lstm.hidden_size
-        x_proj = torch.addmm(self.lstm.bias_ih_l0 + self.lstm.bias_hh_l0, feats, self.lstm.weight_ih_l0.t())
+        bias = self.lstm.bias_ih_l0 + self.lstm.bias_hh_l0
+        if feats.is_cuda:
+            # HIP path: split-K input projection + fused cell kernels (fused.py)
+            x_proj = (SplitKLinear.apply(feats, self.lstm.weight_ih_l0, bias) if torch.is_grad_enabled()
+                      else torch.addmm(bias, feats, self.lstm.weight_ih_l0.t()))
+            keep = (1.0 - done).float().view(-1, B)
+            hid, hT, cT = LSTMSequence.apply(x_proj.view(-1, B, 4 * H), h[0], c[0], keep, self.lstm.weight_hh_l0)
+            return hid.view(-1, H), (hT.unsqueeze(0), cT.unsqueeze(0))
+        x_proj = torch.addmm(bias, feats, self.lstm.weight_ih_l0.t())
         x_proj = x_proj.view(-1, B, 4 * H)
         keep = (1.0 - done).view(-1, B, 1)
         h, c = h[0], c[0]
@@ -101,7 +113,7 @@ class LSTMActor(nn.Module):
 
     def forward(self, state, lstm_state, done, action=None):
         hidden, lstm_state = self.get_states(state, lstm_state, done)
-        mean = self.actor_mean(hidden)
+        mean = self.actor_mean(hidden)    # 128 -> 4: too small for the split-K path
         return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha), lstm_state)
 
 
@@ -129,4 +141,4 @@ class Critic(nn.Module):
         )
 
     def forward(self, state):
-        return self.critic(state)
+        return run_mlp(self.critic, state)

@@ -96,3 +96,43 @@ def test_training_loop_runs(tmp_path, algo, env, n):
     res = main(["--algo", algo, "--env", env, "--num_envs", str(n), "--total_steps", str(n * 20), "--play",
                 "--checkpoint", str(tmp_path / "ck" / name), "--quiet"])
     assert np.isfinite(res["mean_reward"])
+
+
+def test_fused_lstm_and_splitk_gradients_match_torch():
+    """Fused HIP LSTM (forward + BPTT) and split-K weight gradients == torch autograd through the
+    reference's per-step nn.LSTM loop (model.py:34-50), same parameters, with done masks."""
+    from ouzelum_amd.learners.models import LSTMActor
+    from ouzelum_amd.spaces import Box
+    torch.manual_seed(1)
+    a = LSTMActor(Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))).cuda()
+    T, B = 16, 1024                       # 16384 rows: the split-K path is taken
+    x = torch.randn(T * B, 13, device="cuda")
+    dn = (torch.rand(T * B, device="cuda") < 0.1).float()
+    h0 = torch.randn(1, B, 128, device="cuda") * 0.5
+    c0 = torch.randn(1, B, 128, device="cuda") * 0.5
+    w_out = torch.randn(T * B, 128, device="cuda")
+
+    def loss_fused():
+        hid, (h1, c1) = a.get_states(x, (h0, c0), dn)
+        return (hid * w_out).sum() + h1.sum() * 0.5 + c1.sum() * 0.25
+
+    def loss_ref():
+        feats = a.network(x).reshape(T, B, 256)
+        st = (h0, c0)
+        outs = []
+        for t in range(T):
+            keep = (1.0 - dn.reshape(T, B)[t]).view(1, -1, 1)
+            o, st = a.lstm(feats[t].unsqueeze(0), (keep * st[0], keep * st[1]))
+            outs.append(o)
+        hid = torch.flatten(torch.cat(outs), 0, 1)
+        return (hid * w_out).sum() + st[0].sum() * 0.5 + st[1].sum() * 0.25
+
+    grads = []
+    for fn in (loss_fused, loss_ref):
+        a.zero_grad()
+        fn().backward()
+        grads.append({k: p.grad.clone() for k, p in a.named_parameters() if p.grad is not None})
+    assert set(grads[0]) == set(grads[1])
+    errs = {k: float((grads[0][k] - grads[1][k]).abs().max() / grads[1][k].abs().max().clamp_min(1e-6))
+            for k in grads[1]}
+    assert max(errs.values()) < 2e-4, errs
