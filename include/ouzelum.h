@@ -160,6 +160,23 @@ typedef struct ouz_buffers {
   uint8_t* timeouts;        /* [num_envs] bool time_outs                         */
 } ouz_buffers;
 
+/* VecTask domain-randomisation noise on observations / actions (tasks/base/
+ * vec_task.py:576-646 "observations" / "actions" entries; applied in step() before
+ * the clamps, :323-325,352-353).  noise = corr * b_c + a_c + fresh * b + a (gaussian,
+ * a = mu, b = the reference's "var", used there as a standard deviation) or
+ * corr * (hi_c - lo_c) + lo_c + U[0,1) * (hi - lo) + lo (uniform); corr ~ N(0,1) is drawn
+ * once per env element and kept (the reference's params['corr']); x + noise (additive) or
+ * x * noise (scaling).  schedule: 0 none, 1 linear over schedule_steps, 2 constant (off
+ * until schedule_steps), evaluated at the current step. */
+typedef struct ouz_dr_noise {
+  int32_t distribution;     /* 0 off, 1 gaussian, 2 uniform                       */
+  int32_t operation;        /* 0 additive, 1 scaling                              */
+  float range[2];           /* (mu, sigma) or (lo, hi)                            */
+  float range_correlated[2];
+  int32_t schedule;         /* 0 none, 1 linear, 2 constant                       */
+  int32_t schedule_steps;
+} ouz_dr_noise;
+
 typedef struct ouz_task_info {
   int32_t max_episode_length;
   float z_die;
@@ -205,6 +222,8 @@ int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream);
  * step s.  capacity >= 64 (the fused rollout runs waves up to 32 steps apart);
  * capacity 0 disables.  The host must read slots before they are reused. */
 int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity);
+/* target 0 = observations, 1 = actions; dr == NULL or distribution 0 disables. */
+int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr);
 int64_t ouz_get_step(const ouz_env* env);
 int ouz_set_step(ouz_env* env, int64_t step);
 

@@ -541,6 +541,59 @@ def pomdp_apply(x, mode, prob, seed, env_ids, step, site, batch_tag=0, per_env_c
 
 
 # ---------------------------------------------------------------------------
+# VecTask DR noise lambdas (a22): tasks/base/vec_task.py:576-646, applied in step() :323-325,351-353
+# ---------------------------------------------------------------------------
+DRN_DIST = {"gaussian": 1, "uniform": 2}
+DRN_OP = {"additive": 0, "scaling": 1}
+DRN_SCHED = {None: 0, "linear": 1, "constant": 2}
+
+
+def _normal_from(a, b, second):
+    u1 = ((a >> np.uint32(8)).astype(np.float64) + 1.0) / 16777216.0
+    u2 = rng.u32_to_unit_f32(b).astype(np.float64)
+    r = np.sqrt(-2.0 * np.log(u1))
+    return r * (np.sin(2 * math.pi * u2) if second else np.cos(2 * math.pi * u2))
+
+
+def dr_noise_apply(x, p, seed, env_ids, step, stream):
+    """One noise_lambda call.  p: dict with distribution/operation/range/range_correlated/
+    schedule/schedule_steps (the reference's dr_params entry, names mapped to ints)."""
+    if not p or p.get("distribution", 0) == 0:
+        return x
+    s = 1.0
+    if p["schedule"] == 1:
+        s = min(step, p["schedule_steps"]) / p["schedule_steps"]
+    elif p["schedule"] == 2:
+        s = 0.0 if step < p["schedule_steps"] else 1.0
+    a, b = (float(np.float32(v)) for v in p["range"])
+    ac, bc = (float(np.float32(v)) for v in p["range_correlated"])
+    add, gauss = p["operation"] == 0, p["distribution"] == 1
+    if add:
+        a, b, ac, bc = a * s, b * s, ac * s, bc * s
+    elif gauss:
+        b, a, bc, ac = b * s, a * s + (1 - s), bc * s, ac * s + (1 - s)
+    else:
+        a, b, ac, bc = (v * s + (1 - s) for v in (a, b, ac, bc))
+    out = np.array(x, dtype=np.float64, copy=True)
+    d = out.shape[1]
+    for g in range((d + 3) // 4):
+        f = rng.draw_u32(seed, env_ids, step, stream, g)
+        c = rng.draw_u32(seed, env_ids, rng.INIT_STEP, stream, g)
+        for k in range(4):
+            e = g * 4 + k
+            if e >= d:
+                break
+            pair = k & 2
+            corr = _normal_from(c[pair], c[pair + 1], k & 1)
+            if gauss:
+                n = corr * bc + ac + _normal_from(f[pair], f[pair + 1], k & 1) * b + a
+            else:
+                n = corr * (bc - ac) + ac + rng.u32_to_unit_f32(f[k]).astype(np.float64) * (b - a) + a
+            out[:, e] = out[:, e] + n if add else out[:, e] * n
+    return out
+
+
+# ---------------------------------------------------------------------------
 # Task presets (SURVEY §8a; BASELINE.json configs)
 # ---------------------------------------------------------------------------
 CTRL_RL, CTRL_LEE_TRUE, CTRL_LEE_EST = 0, 1, 2
@@ -611,6 +664,8 @@ class EnvConfig:
     thrust_max: float = 2000.0   # ouzelum.py:91
     thrust_rate: float = 2000.0  # ouzelum.py:237
     max_episode_length: int = 0  # 0 -> task default
+    dr_obs: dict | None = None   # VecTask DR noise on observations / actions (dr_noise_apply's p)
+    dr_act: dict | None = None
 
 
 def env_task_ids(cfg: EnvConfig):
@@ -707,7 +762,9 @@ class OracleEnv:
         t = self.sim_step
         dt = cfg.dt
         dtype = self.dt_
-        a = np.clip(np.asarray(actions, dtype=dtype), -1.0, 1.0)        # vec_task.py:327
+        a = np.asarray(actions, dtype=dtype)
+        a = dr_noise_apply(a, cfg.dr_act, cfg.seed, self.gid, t, rng.RNG_DRN_ACT)   # vec_task.py:323-325
+        a = np.clip(a, -1.0, 1.0)                                        # vec_task.py:327
         rst = self.reset_buf != 0
         ids = self.gid
         f_b = np.zeros((n, 3), dtype)
@@ -778,6 +835,7 @@ class OracleEnv:
         self.rew = rew
         self.reset_buf = reset
         self.timeouts = (self.progress >= maxlen - 1) & (self.reset_buf != 0)   # vec_task.py:345
+        obs = dr_noise_apply(obs, cfg.dr_obs, cfg.seed, ids, t, rng.RNG_DRN_OBS)  # vec_task.py:351-352
         self.obs = np.clip(obs, -5.0, 5.0)                                       # vec_task.py:353
         self.sim_step += 1
         return self.obs, self.rew, self.reset_buf, self.timeouts

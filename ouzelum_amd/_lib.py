@@ -55,6 +55,12 @@ class OuzConfig(ctypes.Structure):
     ]
 
 
+class OuzDrNoise(ctypes.Structure):
+    _fields_ = [("distribution", ctypes.c_int32), ("operation", ctypes.c_int32), ("range", ctypes.c_float * 2),
+                ("range_correlated", ctypes.c_float * 2), ("schedule", ctypes.c_int32),
+                ("schedule_steps", ctypes.c_int32)]
+
+
 class OuzBuffers(ctypes.Structure):
     _fields_ = [("fstate", ctypes.c_void_p), ("istate", ctypes.c_void_p), ("obs", ctypes.c_void_p),
                 ("rew", ctypes.c_void_p), ("reset", ctypes.c_void_p), ("timeouts", ctypes.c_void_p)]
@@ -90,6 +96,7 @@ SIGNATURES = {
     "ouz_reset_all": (_I, [_P, _P]),
     "ouz_episode_stats": (_I, [_P, _P, _I, _P]),
     "ouz_set_trace": (_I, [_P, _P, _P, _I, _I]),
+    "ouz_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
     "ouz_get_step": (_I64, [_P]),
     "ouz_set_step": (_I, [_P, _I64]),
     "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),

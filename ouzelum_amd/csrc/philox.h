@@ -21,6 +21,8 @@ enum RngStream : uint32_t {
   RNG_TRAJ = 3,
   RNG_DR = 4,
   RNG_FAULT = 5,
+  RNG_DRN_OBS = 6,  // VecTask DR noise on observations (vec_task.py:576-646)
+  RNG_DRN_ACT = 7,  // ... on actions
   RNG_POMDP = 16,  // + call site
 };
 constexpr uint32_t BATCH_ENV = 0xFFFFFFFFu;

@@ -81,6 +81,7 @@ struct StepArgs {
   uint64_t n_total;
   uint64_t seed;
   int32_t track_episodes;
+  ouz_dr_noise drn[2];         // VecTask DR noise: [0] observations, [1] actions
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
   uint32_t* trace_resets;      // [trace_cap] envs reset at the start of each step
   int32_t trace_env, trace_cap;
@@ -146,6 +147,53 @@ __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int 
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         if (g * 4 + k < D) x[g * 4 + k] *= uniform_f32(w4[k], tp.noise_lo, tp.noise_hi);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// VecTask DR noise lambdas (tasks/base/vec_task.py:576-646), counter-RNG normals (Box-Muller)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float normal_from(uint32_t a, uint32_t b, bool second) {
+  const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);    // (0, 1]
+  const float u2 = unit_f32(b);
+  const float r = sqrtf(-2.0f * logf(u1));
+  float sn, cs;
+  sincosf(6.28318530717958647692f * u2, &sn, &cs);
+  return second ? r * sn : r * cs;
+}
+
+// D values of env gid (D <= 16): noise drawn from `stream`, subs 0..3 fresh (step-keyed), corr at INIT_STEP
+template <int D>
+__device__ __forceinline__ void dr_noise_apply(float* x, const ouz_dr_noise& p, uint64_t seed, uint32_t gid,
+                                               uint32_t step, uint32_t stream) {
+  if (p.distribution == 0) return;
+  float s = 1.0f;                                                        // schedule (vec_task.py:584-589)
+  if (p.schedule == 1) s = fminf((float)step, (float)p.schedule_steps) / (float)p.schedule_steps;
+  else if (p.schedule == 2) s = step < (uint32_t)p.schedule_steps ? 0.0f : 1.0f;
+  float a = p.range[0], b = p.range[1], ac = p.range_correlated[0], bc = p.range_correlated[1];
+  const bool add = p.operation == 0, gauss = p.distribution == 1;
+  if (add) {
+    a *= s; b *= s; ac *= s; bc *= s;
+  } else if (gauss) {                                                    // :601-606
+    b *= s; a = a * s + (1.0f - s); bc *= s; ac = ac * s + (1.0f - s);
+  } else {                                                               // :629-633
+    a = a * s + (1.0f - s); b = b * s + (1.0f - s); ac = ac * s + (1.0f - s); bc = bc * s + (1.0f - s);
+  }
+#pragma unroll
+  for (int g = 0; g < (D + 3) / 4; ++g) {
+    const U4 f = draw(seed, gid, step, stream, (uint32_t)g);
+    const U4 c = draw(seed, gid, INIT_STEP, stream, (uint32_t)g);
+    const uint32_t fw[4] = {f.x, f.y, f.z, f.w}, cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = g * 4 + k;
+      if (e >= D) break;
+      const float corr = normal_from(cw[k & 2], cw[(k & 2) + 1], k & 1);
+      float n;
+      if (gauss) n = corr * bc + ac + normal_from(fw[k & 2], fw[(k & 2) + 1], k & 1) * b + a;
+      else n = corr * (bc - ac) + ac + unit_f32(fw[k]) * (b - a) + a;
+      x[e] = add ? x[e] + n : x[e] * n;
     }
   }
 }
@@ -374,6 +422,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     float4 act = reinterpret_cast<const float4*>(sc.actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
     float av[4] = {act.x, act.y, act.z, act.w};
+    dr_noise_apply<4>(av, a.drn[1], a.seed, gid, sc.step, RNG_DRN_ACT);   // vec_task.py:323-325
     float eff[4];
     const bool on = tp.fault && S.progress >= S.fonset;
 #pragma unroll
@@ -534,6 +583,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
   ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
   ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
   pomdp_apply<13>(ob, tp, task, a, sc, gid, SITE_OBS, false);
+  dr_noise_apply<13>(ob, a.drn[0], a.seed, gid, sc.step, RNG_DRN_OBS);   // vec_task.py:351-352
 #pragma unroll
   for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
@@ -943,6 +993,7 @@ using namespace ouz;
 static_assert(sizeof(ouz_config) == 88, "ctypes OuzConfig mirror (ouzelum_amd/_lib.py)");
 static_assert(sizeof(ouz_buffers) == 48, "ctypes OuzBuffers mirror");
 static_assert(sizeof(ouz_task_info) == 32, "ctypes OuzTaskInfo mirror");
+static_assert(sizeof(ouz_dr_noise) == 32, "ctypes OuzDrNoise mirror");
 
 namespace {
 thread_local std::string g_err;
@@ -1285,6 +1336,17 @@ int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_inde
   env->args.trace_resets = resets;
   env->args.trace_env = env_index;
   env->args.trace_cap = capacity;
+  return OUZ_OK;
+}
+
+int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr) {
+  if (!env || target < 0 || target > 1) return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad env or target");
+  ouz_dr_noise p{};
+  if (dr) p = *dr;
+  if (p.distribution < 0 || p.distribution > 2 || p.operation < 0 || p.operation > 1 || p.schedule < 0 ||
+      p.schedule > 2 || (p.schedule && p.schedule_steps <= 0))
+    return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad distribution / operation / schedule");
+  env->args.drn[target] = p;
   return OUZ_OK;
 }
 

@@ -229,6 +229,34 @@ class QuadVecTask:
                 "ouz_episode_stats")
         return self._stats_buf
 
+    _DRN_DIST = {"gaussian": 1, "uniform": 2}
+    _DRN_OP = {"additive": 0, "scaling": 1}
+    _DRN_SCHED = {None: 0, "linear": 1, "constant": 2}
+
+    def apply_randomizations(self, dr_params):
+        """The non-physical part of VecTask.apply_randomizations (vec_task.py:576-646): the
+        "observations" / "actions" noise lambdas, evaluated inside the step kernel with the
+        counter RNG.  Physical entries (sim_params, actor_params) are not implemented: the drone
+        tasks disable them (EKFLeeLanded.yaml:48-49); mass / inertia / thrust DR is QuadTracking's."""
+        unknown = set(dr_params) - {"observations", "actions", "frequency"}
+        if unknown:
+            raise NotImplementedError(f"randomization entries {sorted(unknown)} are not implemented on the HIP path")
+        for target, key in ((0, "observations"), (1, "actions")):
+            L.check(L.lib.ouz_set_dr_noise(self._env, target, self._dr_struct(dr_params.get(key))),
+                    "ouz_set_dr_noise")
+
+    def _dr_struct(self, p):
+        s = L.OuzDrNoise()
+        if not p:
+            return s
+        s.distribution = self._DRN_DIST[p["distribution"]]
+        s.operation = self._DRN_OP[p["operation"]]
+        s.range[0], s.range[1] = p["range"]
+        s.range_correlated[0], s.range_correlated[1] = p.get("range_correlated", [0.0, 0.0])
+        s.schedule = self._DRN_SCHED[p.get("schedule")]
+        s.schedule_steps = int(p.get("schedule_steps", 0))
+        return s
+
     def enable_trace(self, env_index=0, capacity=4096):
         """Record (p, target, v) of one env and the number of envs reset at every step, written by
         the step kernel itself (``ouz_set_trace``).  Read with ``trace_since``; see outputs.py."""

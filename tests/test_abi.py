@@ -50,6 +50,7 @@ def test_struct_layout(L):
     # must equal the static_asserts in quad_kernels.hip
     assert ctypes.sizeof(L.OuzConfig) == 88
     assert ctypes.sizeof(L.OuzBuffers) == 48
+    assert ctypes.sizeof(L.OuzTaskInfo) == 32 and ctypes.sizeof(L.OuzDrNoise) == 32
 
 
 def test_argument_validation_without_gpu(L):
