@@ -38,7 +38,9 @@ RING = 16
 # Algorithmic bytes per env-step of quad_step_kernel<TASK>: every
 # field the kernel must read and write per env, SoA f32 / i32, obs AoS f32,
 # reset i64, timeouts u8.  Reset-only and done-only traffic is excluded.
-_CORE = 8 + 52 + 4 + 52 + 4 + 52 + 4 + 8 + 1   # reset r, p/q/v/w r+w, progress r+w, obs w, rew w, reset w, timeouts w
+# reset r, p/q/v/w r+w, progress r+w, obs w, rew w, timeouts r (reset / timeouts are written only
+# when an env is or was done: a few % of env-steps, excluded like the other done-only traffic)
+_CORE = 8 + 52 + 4 + 52 + 4 + 52 + 4 + 1
 BYTES_PER_ENV_STEP = {
     "LeeLanded": _CORE,
     # + random-goal target (12 r/w), rotor thrusts (16 r/w), actions (16 r)

@@ -81,7 +81,8 @@ struct StepArgs {
   uint64_t n_total;
   uint64_t seed;
   int32_t track_episodes;
-  ouz_dr_noise drn[2];         // VecTask DR noise: [0] observations, [1] actions
+  const ouz_dr_noise* drn;     // VecTask DR noise params in device memory: [0] observations, [1] actions
+  int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
   uint32_t* trace_resets;      // [trace_cap] envs reset at the start of each step
   int32_t trace_env, trace_cap;
@@ -258,6 +259,7 @@ struct EnvRegs {
   Q4 q;
   int32_t progress;
   bool rst;                       // reset_buf != 0: lazy reset at the start of the next step
+  bool flags_clear;               // reset_buf == 0 and time_outs == 0 in the buffers (emit may skip them)
   V3 target;                      // TGT_GOAL: stored random goal
   float thrust[4];                // CTRL_RL
   int32_t frot, fonset;           // fault
@@ -280,6 +282,7 @@ struct EnvRegs {
 template <int CTRL, int TGT>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S) {
   S.rst = (a.reset + S.T.first)[S.T.l] != 0;
+  S.flags_clear = !S.rst && (a.timeouts + S.T.first)[S.T.l] == 0;   // issued with the state loads
   S.p = ld3(S.T, OUZ_F_P);
   S.q = Q4{ld(S.T, OUZ_F_Q), ld(S.T, OUZ_F_Q + 1), ld(S.T, OUZ_F_Q + 2), ld(S.T, OUZ_F_Q + 3)};
   S.v = ld3(S.T, OUZ_F_V);
@@ -422,7 +425,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     float4 act = reinterpret_cast<const float4*>(sc.actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
     float av[4] = {act.x, act.y, act.z, act.w};
-    dr_noise_apply<4>(av, a.drn[1], a.seed, gid, sc.step, RNG_DRN_ACT);   // vec_task.py:323-325
+    if (a.drn_mask & 2) dr_noise_apply<4>(av, a.drn[1], a.seed, gid, sc.step, RNG_DRN_ACT);   // vec_task.py:323-325
     float eff[4];
     const bool on = tp.fault && S.progress >= S.fonset;
 #pragma unroll
@@ -583,7 +586,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
   ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
   ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
   pomdp_apply<13>(ob, tp, task, a, sc, gid, SITE_OBS, false);
-  dr_noise_apply<13>(ob, a.drn[0], a.seed, gid, sc.step, RNG_DRN_OBS);   // vec_task.py:351-352
+  if (a.drn_mask & 1) dr_noise_apply<13>(ob, a.drn[0], a.seed, gid, sc.step, RNG_DRN_OBS);   // vec_task.py:351-352
 #pragma unroll
   for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
@@ -627,7 +630,7 @@ struct OutPtrs {
 };
 
 __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, int n, bool valid, const float* ob,
-                                     float rew, bool rs, bool to, bool direct) {
+                                     float rew, bool rs, bool to, bool direct, bool keep_flags = false) {
   const uint32_t lane = (uint32_t)i & 63u;
   const uint32_t first = wave_tile(i) * 64u;   // wave-uniform: output bases live in SGPRs
   if (direct) {   // wave shared by two tasks (misaligned mixed shard): plain per-lane stores
@@ -644,8 +647,13 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
 #pragma unroll
     for (int k = 0; k < OUZ_NUM_OBS; ++k) wave_lds[lane * OUZ_NUM_OBS + k] = ob[k];
     (o.rew + first)[lane] = rew;
-    (o.reset + first)[lane] = rs ? 1 : 0;
-    (o.timeouts + first)[lane] = to ? 1 : 0;
+    // keep_flags: reset_buf and time_outs held 0 at the start of the step (read with the state); if
+    // the env is still not done both buffers already hold this step's values: skip the 9-byte write
+    // (a time-out left over from a manually cleared reset_buf is rewritten)
+    if (!(keep_flags && !rs)) {
+      (o.reset + first)[lane] = rs ? 1 : 0;
+      (o.timeouts + first)[lane] = to ? 1 : 0;
+    }
   }
   wave_lds_sync();
   const uint32_t m = min(64u, (uint32_t)(n - (int)first));
@@ -693,16 +701,19 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     for (int k = 0; k < OUZ_NUM_OBS; ++k) ob[k] = S.p.x * k;
 #else
     const bool did_reset = valid && S.rst;
+    const bool flags_clear = valid && S.flags_clear;
     if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
     trace_count(a, ctx[0].step, did_reset, i);
 #endif
-    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
   } else {
     for (int k = 0; k < K; ++k) {
       float ob[OUZ_NUM_OBS];
       float rew = 0.0f;
       bool rs = false, to = false;
       const bool did_reset = valid && S.rst;
+      // in the loop the buffers hold the previous step's flags: clear iff it was not done
+      const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
       if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
       trace_count(a, ctx[k].step, did_reset, i);
       OutPtrs o = outs[0];
@@ -714,7 +725,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
         emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
         if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
       } else {
-        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
       }
     }
   }
@@ -1026,6 +1037,8 @@ struct ouz_env {
   int64_t step;
   float2* wp_tab;   // device waypoint tables
   double* stats_partials;    // [kStatsMaxBlocks][3] per-block partials of episode_stats_kernel
+  ouz_dr_noise* drn_dev;     // [2] DR noise params (read by the step kernel only when enabled)
+  ouz_dr_noise drn_host[2];
   uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
 };
@@ -1109,6 +1122,9 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
                 "hipMalloc(stats)");
   if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
   e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
+  r = hip_check(hipMalloc(&e->drn_dev, 2 * sizeof(ouz_dr_noise)), "hipMalloc(dr noise)");
+  if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
+  std::memset(e->drn_host, 0, sizeof(e->drn_host));
   r = hip_check(hipMemset(e->stats_ticket, 0, sizeof(uint32_t)), "hipMemset(stats)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   StepArgs& a = e->args;
@@ -1153,6 +1169,7 @@ int ouz_destroy(ouz_env* env) {
   if (!env) return OUZ_OK;
   if (env->wp_tab) (void)hipFree(env->wp_tab);
   if (env->stats_partials) (void)hipFree(env->stats_partials);
+  if (env->drn_dev) (void)hipFree(env->drn_dev);
   delete env;
   return OUZ_OK;
 }
@@ -1346,7 +1363,12 @@ int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr) {
   if (p.distribution < 0 || p.distribution > 2 || p.operation < 0 || p.operation > 1 || p.schedule < 0 ||
       p.schedule > 2 || (p.schedule && p.schedule_steps <= 0))
     return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad distribution / operation / schedule");
-  env->args.drn[target] = p;
+  env->drn_host[target] = p;
+  int r = hip_check(hipMemcpy(env->drn_dev, env->drn_host, sizeof(env->drn_host), hipMemcpyHostToDevice),
+                    "hipMemcpy(dr noise)");
+  if (r) return r;
+  env->args.drn = env->drn_dev;
+  env->args.drn_mask = (env->drn_host[0].distribution ? 1 : 0) | (env->drn_host[1].distribution ? 2 : 0);
   return OUZ_OK;
 }
 
