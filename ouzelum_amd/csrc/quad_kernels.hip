@@ -269,10 +269,7 @@ struct EnvRegs {
   EkfQ eq;
   float eP[10], px[9], pP[45];
   float2 plat;                    // platform xy (TGT_TRAJ state; (0, 0) for TGT_PLATFORM)
-  float plat_th;                  // TGT_TRAJ: husky heading
   float2 plat_v;                  // this step's platform velocity (deck contact)
-  int32_t ttype, tidx;
-  float sd;
   int32_t land_flag;              // -1: not loaded (only needed on reset / landing)
   int32_t landings_add, ep_cnt_add, ep_len_add;
   float ep_ret, ep_sum_add;
@@ -317,13 +314,9 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   }
   if constexpr (TGT == TGT_TRAJ) {
     S.plat = make_float2(ld(S.T, OUZ_F_PLAT), ld(S.T, OUZ_F_PLAT + 1));
-    S.plat_th = ld(S.T, OUZ_F_PLAT_HEADING);
-    S.ttype = ldi(S.T, OUZ_I_TRAJ_TYPE);
-    S.tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
-    S.sd = ld(S.T, OUZ_F_TRAJ_SD);
+
   } else {
     S.plat = make_float2(0.0f, 0.0f);
-    S.plat_th = 0.0f;
   }
   S.plat_v = make_float2(0.0f, 0.0f);
 }
@@ -364,10 +357,51 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
     for (int k = 0; k < 45; ++k) st(S.T, OUZ_F_PV_P + k, S.pP[k]);
   }
   if constexpr (TGT == TGT_TRAJ) {
-    st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y); st(S.T, OUZ_F_PLAT_HEADING, S.plat_th);
-    sti(S.T, OUZ_I_TRAJ_IDX, S.tidx);
-    if (S.dirty & D_TRAJ) { sti(S.T, OUZ_I_TRAJ_TYPE, S.ttype); st(S.T, OUZ_F_TRAJ_SD, S.sd); }
+    st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y);
   }
+}
+
+// The husky following its waypoints (landing.py:319-364) as a kinematic differential-drive unicycle
+// (oracle OracleEnv._platform_step).  Runs right before the integrator: nothing earlier in the step
+// reads the platform (the target comes from the previous step's position), so the trajectory state
+// (type, index, scale, heading) is loaded, advanced and stored here and never held across the
+// estimator's register peak.
+template <int CTRL, int TGT>
+__device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& sc, uint32_t gid,
+                                              EnvRegs<CTRL, TGT>& S) {
+  const EnvConsts& c = a.c;
+  int ttype = ldi(S.T, OUZ_I_TRAJ_TYPE), tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
+  float sd = ld(S.T, OUZ_F_TRAJ_SD), th = ld(S.T, OUZ_F_PLAT_HEADING);
+  float2 wpp = traj_point(a, ttype, tidx, sd);
+  float dx = wpp.x - S.plat.x, dy = wpp.y - S.plat.y;
+  if (sqrtf(dx * dx + dy * dy) < 0.2f) tidx += 1;
+  const int len = ttype == 0 ? kTrajLen[0] : (ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
+  if (tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
+    U4 r = draw(a.seed, gid, sc.step, RNG_TRAJ);
+    ttype = (int)(r.x % 3u);
+    sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
+    tidx = 0;
+    sti(S.T, OUZ_I_TRAJ_TYPE, ttype);
+    st(S.T, OUZ_F_TRAJ_SD, sd);
+  }
+  // differential_drive (utils/controllers.py:15-43, gains (3, 1000) landing.py:361) on a
+  // kinematic unicycle; wheel speeds saturate at plat_speed / wheel radius (15 rad/s)
+  wpp = traj_point(a, ttype, tidx, sd);
+  dx = wpp.x - S.plat.x; dy = wpp.y - S.plat.y;
+  float dth = map_to_pi(atan2f(dy, dx) - map_to_pi(th));
+  if (fabsf(dth) < kDriveAngThresh) dth = 0.0f;
+  float lin = sqrtf(dx * dx + dy * dy) * kDriveGainLin, ang = dth * kDriveGainAng;
+  const float wl = (2.0f * lin + ang * kWheelBase) / (2.0f * kWheelRadius);
+  const float wr = (2.0f * lin - ang * kWheelBase) / (2.0f * kWheelRadius);
+  const float mx = fmaxf(fabsf(wl), fabsf(wr)), max_w = c.plat_speed / kWheelRadius;
+  if (mx > max_w) { const float scl = max_w / mx; lin *= scl; ang *= scl; }
+  th = map_to_pi(th + ang * c.dt);
+  float sn, cs;
+  sincosf(th, &sn, &cs);
+  S.plat_v = make_float2(lin * cs, lin * sn);
+  S.plat.x += S.plat_v.x * c.dt; S.plat.y += S.plat_v.y * c.dt;
+  sti(S.T, OUZ_I_TRAJ_IDX, tidx);
+  st(S.T, OUZ_F_PLAT_HEADING, th);
 }
 
 // ---------------------------------------------------------------------------
@@ -467,36 +501,6 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
   } else {
     // ---- AHRS-EKF + PV-KF + waypoint guidance + Lee (ekf_lee_landed.py:308-530) ----
     const bool conv = sc.step < (uint32_t)c.conv_time;
-    if constexpr (TGT == TGT_TRAJ) {
-      // kinematic stand-in for the husky waypoint follower (landing.py:319-364)
-      float2 wpp = traj_point(a, S.ttype, S.tidx, S.sd);
-      float dx = wpp.x - S.plat.x, dy = wpp.y - S.plat.y;
-      if (sqrtf(dx * dx + dy * dy) < 0.2f) S.tidx += 1;
-      int len = S.ttype == 0 ? kTrajLen[0] : (S.ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
-      if (S.tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
-        U4 r = draw(a.seed, gid, sc.step, RNG_TRAJ);
-        S.ttype = (int)(r.x % 3u);
-        S.sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
-        S.tidx = 0;
-        S.dirty |= D_TRAJ;
-      }
-      // differential_drive (utils/controllers.py:15-43, gains (3, 1000) landing.py:361) on a
-      // kinematic unicycle; wheel speeds saturate at plat_speed / wheel radius (15 rad/s)
-      wpp = traj_point(a, S.ttype, S.tidx, S.sd);
-      dx = wpp.x - S.plat.x; dy = wpp.y - S.plat.y;
-      float dth = map_to_pi(atan2f(dy, dx) - map_to_pi(S.plat_th));
-      if (fabsf(dth) < kDriveAngThresh) dth = 0.0f;
-      float lin = sqrtf(dx * dx + dy * dy) * kDriveGainLin, ang = dth * kDriveGainAng;
-      const float wl = (2.0f * lin + ang * kWheelBase) / (2.0f * kWheelRadius);
-      const float wr = (2.0f * lin - ang * kWheelBase) / (2.0f * kWheelRadius);
-      const float mx = fmaxf(fabsf(wl), fabsf(wr)), max_w = c.plat_speed / kWheelRadius;
-      if (mx > max_w) { const float sc = max_w / mx; lin *= sc; ang *= sc; }
-      S.plat_th = map_to_pi(S.plat_th + ang * c.dt);
-      float sn, cs;
-      sincosf(S.plat_th, &sn, &cs);
-      S.plat_v = make_float2(lin * cs, lin * sn);
-      S.plat.x += S.plat_v.x * c.dt; S.plat.y += S.plat_v.y * c.dt;
-    }
     V3 lin_acc = v3((S.v.x - S.prev_v.x) / c.dt, (S.v.y - S.prev_v.y) / c.dt, (S.v.z - S.prev_v.z) / c.dt);
     lin_acc.z += 9.8f;                                 // aliasing quirk (ekf_lee_landed.py:366-367)
     EkfQ qt{S.q.w, S.q.x, S.q.y, S.q.z};
@@ -566,6 +570,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
+    if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);
     integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
               DeckContact{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y});
   }
