@@ -426,3 +426,23 @@ def test_vectask_dr_noise_parity(ouz, obs_p, act_p):
         assert_close(f"drn@{k} thrust", g["thrust"], r["thrust"], 1e-3, 1e-6)
     with pytest.raises(NotImplementedError):
         env.apply_randomizations({"sim_params": {}})
+
+
+@pytest.mark.parametrize("task", ["QuadTracking", "QuadMixed"])
+def test_large_n_occupancy_variant_matches(ouz, task):
+    """Above 65 536 envs the estimator tasks launch the 2-waves-per-SIMD kernel variant; it runs the
+    same step body, so 70 016 envs in one env reproduce two 35 008-env shards bit for bit."""
+    from ouzelum_amd import _lib as L
+    n = 70016
+    full = ouz.make(seed=12, task=task, num_envs=n, sim_device="cuda:0", convergence_time=5)
+    halves = [ouz.make(seed=12, task=task, num_envs=n // 2, sim_device="cuda:0", env_id_offset=r * n // 2,
+                       num_envs_total=n, convergence_time=5) for r in range(2)]
+    g = torch.Generator(device="cuda").manual_seed(4)
+    for _ in range(12):
+        a = torch.rand((n, 4), device="cuda", generator=g) * 2 - 1
+        full.step(a)
+        halves[0].step(a[: n // 2].contiguous())
+        halves[1].step(a[n // 2:].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(full.frows(0, L.F_COUNT), torch.cat([h.frows(0, L.F_COUNT) for h in halves], 1))
+    assert torch.equal(full.obs_buf, torch.cat([h.obs_buf for h in halves], 0))
