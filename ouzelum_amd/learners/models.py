@@ -118,14 +118,16 @@ class LSTMActor(nn.Module):
 
 
 def _policy_head(mean, logstd, action, rpo_alpha):
+    # validate_args=False: the default argument check is a device->host sync on every call (and
+    # cannot be captured in a hipGraph); mean / std are finite by construction
     std = torch.exp(logstd.expand_as(mean))
     if action is None:
-        probs = Normal(mean, std)
+        probs = Normal(mean, std, validate_args=False)
         action = probs.sample()
     else:
         if rpo_alpha > 0.0:   # RPO: perturb the mean for the policy update (RPO-LSTM/model.py:61-64)
             mean = mean + torch.empty_like(mean).uniform_(-rpo_alpha, rpo_alpha)
-        probs = Normal(mean, std)
+        probs = Normal(mean, std, validate_args=False)
     return action, probs.log_prob(action).sum(1), probs.entropy().sum(1)
 
 

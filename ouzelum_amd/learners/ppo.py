@@ -11,8 +11,7 @@ Differences, all MI355X-side:
 * GAE is one HIP launch (``ouz_gae``) instead of a T-step Python loop; values are
   computed without building an autograd graph (the reference's graph there is
   never used: ``clip_vloss`` is False).
-* Minibatch permutations come from ``torch.randperm`` on the device (no H2D copy of
-  a numpy permutation) and the clip fractions stay on the device until the end of
+* Minibatch permutations come from device RNG (no H2D copy of a numpy permutation) and the clip fractions stay on the device until the end of
   the update (the reference syncs with ``.item()`` every minibatch).
 * Under torchrun (one process per GPU, env ids sharded) the learner is data
   parallel: rank 0's initial weights are broadcast and every optimizer step
@@ -119,6 +118,10 @@ class PPOLearner:
         return gae(rewards, values, dones, next_value, next_done, self.gamma, self.gae_lamda)
 
     # ------------------------------------------------------------------- update
+    def _perm(self, n):
+        """A uniform random permutation from device RNG (no host round trip)."""
+        return torch.argsort(torch.rand(n, device=self.device))
+
     def train(self, obs, pomdps, actions, next_obs, next_done, initial_lstm_state, logprobs, rewards, dones):
         """One PPO update on a (T, N) rollout.  ``pomdps`` are the observations the actor trains on
         (RPO-LSTM trains on the POMDP-corrupted ones, agent.py:83); pass ``obs`` for plain PPO."""
@@ -139,12 +142,12 @@ class PPOLearner:
         stats = {}
         for _ in range(self.update_epochs):
             if self.recurrent:
-                envinds = torch.randperm(N, device=self.device)
+                envinds = self._perm(N)
                 per = N // self.num_minibatches
                 batches = [(flatinds[:, envinds[s:s + per]].reshape(-1), envinds[s:s + per])
                            for s in range(0, N, per)]
             else:
-                b_inds = torch.randperm(T * N, device=self.device)
+                b_inds = self._perm(T * N)
                 batches = [(b_inds[s:s + self.minibatch_size], None) for s in range(0, T * N, self.minibatch_size)]
             for mb_inds, mbenvinds in batches:
                 if self.recurrent:
