@@ -446,3 +446,25 @@ def test_large_n_occupancy_variant_matches(ouz, task):
     torch.cuda.synchronize()
     assert torch.equal(full.frows(0, L.F_COUNT), torch.cat([h.frows(0, L.F_COUNT) for h in halves], 1))
     assert torch.equal(full.obs_buf, torch.cat([h.obs_buf for h in halves], 0))
+
+
+@pytest.mark.parametrize("task,n", [("LeeLanded", 1), ("EKFLeeLanded", 63), ("QuadFault", 65), ("QuadTracking", 130),
+                                    ("QuadMixed", 200), ("LeeLanded", 65537), ("QuadFault", 65537)])
+def test_ragged_sizes_parity(ouz, task, n):
+    """Single env, sub-wave, one-over-a-wave and one-over-the-64-env-block-limit sizes (the 256-lane
+    block path, a 1-lane last wave): state, obs, reward and done masks match the oracle step by step."""
+    kw = {"convergence_time": 3} if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else {}
+    env, o = make_pair(ouz, task, n, seed=21, **kw)
+    rs = np.random.RandomState(8)
+    for k in range(8):
+        a = actions_for(rs, n)
+        gpu_to_oracle(env, o)
+        o.step(a)
+        env.step(torch.as_tensor(a, device="cuda"))
+        g, r = gpu_snapshot(env), oracle_snapshot(o)
+        ok = ~near_threshold(o)
+        assert_close(f"{task}/{n}@{k} p", g["p"][ok], r["p"][ok], 2e-5, 2e-5)
+        assert_close(f"{task}/{n}@{k} obs", g["obs"][ok], r["obs"][ok], 1e-4, 1e-5)
+        assert_close(f"{task}/{n}@{k} rew", g["rew"][ok], r["rew"][ok], 1e-5, 1e-5)
+        np.testing.assert_array_equal(g["reset"][ok], r["reset"][ok])
+        np.testing.assert_array_equal(g["progress"], r["progress"])
