@@ -21,6 +21,9 @@ and writes small ``.npz`` fixtures next to itself.  The fixtures are data
 * Trajectories  isaacgymenvs/utils/trajectories.py.
 * Quaternion rotate (xyzw)  isaacgymenvs/tasks/amp/poselib/poselib/core/rotation3d.py
   (quat_rotate) — the importable twin of isaacgym.torch_utils.quat_rotate.
+* Reward / done  compute_ingenuity_reward of tasks/{ekf_lee_landed,lee_landed,ouzelum}.py and
+  quat_axis of utils/torch_jit_utils.py: those modules import isaacgym at the top, so the two
+  functions' source text is extracted (ast) and executed with torch; quat_rotate is poselib's twin.
 * Husky drive  isaacgymenvs/utils/controllers.py::differential_drive (wheel speeds for random
   poses / targets / headings, landing.py's gains and the defaults).
 * Learner  isaacgymenvs/RPO-LSTM/{model,agent}.py — ``PPO.getGAE`` run unbound on a
@@ -265,6 +268,57 @@ def gen_drive(ref):
     np.savez_compressed(os.path.join(HERE, "drive.npz"), **out)
 
 
+def _extract_function(path, name):
+    """Source text of one top-level function of a reference file whose module cannot be imported
+    (tasks/*.py import isaacgym at the top), without its decorators."""
+    import ast
+    src = open(path).read()
+    for node in ast.parse(src).body:
+        if isinstance(node, ast.FunctionDef) and node.name == name:
+            lines = src.split("\n")[node.lineno - 1:node.end_lineno]
+            return "\n".join(lines)
+    raise KeyError(name)
+
+
+def gen_reward(ref):
+    """compute_ingenuity_reward of ekf_lee_landed.py / lee_landed.py / ouzelum.py, executed from the
+    reference's own source text.  Its quat_axis (utils/torch_jit_utils.py:67-71) is extracted the same
+    way; the isaacgym.torch_utils.quat_rotate it calls is replaced by poselib's twin
+    (tasks/amp/poselib/poselib/core/rotation3d.py, pinned in traj_quat.npz)."""
+    rot = _load("ref_rot3d_r", os.path.join(ref, "isaacgymenvs", "tasks", "amp", "poselib", "poselib", "core",
+                                            "rotation3d.py"))
+    ns = {"torch": torch, "quat_rotate": rot.quat_rotate, "Tensor": torch.Tensor}
+    exec(_extract_function(os.path.join(ref, "isaacgymenvs", "utils", "torch_jit_utils.py"), "quat_axis"), ns)
+    rs = np.random.RandomState(7000)
+    n = 400
+    p = np.concatenate([rs.uniform(-6, 6, (n, 2)), rs.uniform(0.0, 3.0, (n, 1))], 1)
+    p[:20] = rs.uniform(-0.3, 0.3, (20, 3)) + [0, 0, 0.3]          # near the z thresholds
+    tgt = rs.uniform(-3, 3, (n, 3))
+    tgt[20:40] = p[20:40] + rs.normal(0, 1, (20, 3)) * 4.6           # near the distance-8 threshold
+    q = rs.normal(0, 1, (n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    v = rs.normal(0, 1, (n, 3))
+    w = rs.normal(0, 2, (n, 3))
+    prog = rs.randint(0, 2100, n)
+    out = {"p": p, "target": tgt, "q_xyzw": q, "w": w, "progress": prog}
+    T = lambda x: torch.tensor(x, dtype=torch.float32)
+    for task, fname, max_ep in (("ekf", "ekf_lee_landed.py", 700), ("lee", "lee_landed.py", 2000),
+                                ("ouz", "ouzelum.py", 2000)):
+        f = _extract_function(os.path.join(ref, "isaacgymenvs", "tasks", fname), "compute_ingenuity_reward")
+        exec(f, ns)
+        fn = ns["compute_ingenuity_reward"]
+        reset0 = torch.zeros(n, dtype=torch.long)
+        args = [T(p), T(tgt), T(q), T(v), T(w)]
+        if task != "ouz":
+            args.append(torch.zeros(n, 2, 3))                           # forces (unused by the body)
+        args += [reset0, torch.tensor(prog), float(max_ep)]
+        rew, reset = fn(*args)
+        out[f"{task}_rew"] = rew.numpy()
+        out[f"{task}_reset"] = reset.numpy()
+        out[f"{task}_max_ep"] = max_ep
+    np.savez_compressed(os.path.join(HERE, "reward.npz"), **out)
+
+
 def gen_learner(ref):
     d = os.path.join(ref, "isaacgymenvs", "RPO-LSTM")
     model = _load("model", os.path.join(d, "model.py"))      # agent.py does `from model import ...`
@@ -320,4 +374,5 @@ if __name__ == "__main__":
     gen_traj_and_quat(a.ref)
     gen_learner(a.ref)
     gen_drive(a.ref)
+    gen_reward(a.ref)
     print("golden fixtures written to", HERE)

@@ -199,3 +199,18 @@ def test_component_errors(L):
     assert L.lib.ouz_lee_control(7, None, None, None, None, 4, None) == -1
     assert b"Invalid controller" in L.lib.ouz_last_error()
     assert L.lib.ouz_pv_correct(None, None, None, 0, 0.0, None, 4, None) == -1
+
+
+@pytest.mark.parametrize("task,z_die", [("ekf", 0.3), ("ouz", 0.5)])
+def test_reward_kernel_vs_reference_golden(L, golden, task, z_die):
+    """ouz_reward against compute_ingenuity_reward run from the reference's own source text."""
+    g = golden("reward.npz")
+    n = g["p"].shape[0]
+    root = np.concatenate([g["p"], g["q_xyzw"], np.zeros((n, 3)), g["w"]], 1)
+    rew = torch.empty(n, device="cuda")
+    rst = torch.empty(n, dtype=torch.int64, device="cuda")
+    r_d, tg_d, pr_d = t(root), t(g["target"]), t(g["progress"], torch.int32)
+    L.check(L.lib.ouz_reward(r_d.data_ptr(), tg_d.data_ptr(), pr_d.data_ptr(), int(g[f"{task}_max_ep"]), z_die,
+                             rew.data_ptr(), rst.data_ptr(), n, stream()))
+    np.testing.assert_allclose(rew.cpu().numpy(), g[f"{task}_rew"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(rst.cpu().numpy(), g[f"{task}_reset"])

@@ -119,3 +119,17 @@ def test_deck_contact_and_platform_motion():
         tr.step(np.zeros((8, 4)))
     assert np.all(tr.traj_idx + (tr.traj_type * 0) >= 0) and np.abs(tr.plat).max() > 0.5
     assert np.abs(np.sqrt((tr.plat_v ** 2).sum(-1))).max() <= Q.MAX_WHEEL_SPEED * Q.WHEEL_RADIUS + 1e-9
+
+
+@pytest.mark.parametrize("task,z_die", [("ekf", 0.3), ("lee", 0.3), ("ouz", 0.5)])
+def test_reward_matches_reference(golden, task, z_die):
+    """compute_ingenuity_reward executed from the reference's own source (ekf_lee_landed.py:692-723,
+    lee_landed.py:400-430, ouzelum.py:303-332; tests/golden/make_golden.py::gen_reward)."""
+    g = golden("reward.npz")
+    p = g["p"].astype(np.float32).astype(np.float64)
+    tgt = g["target"].astype(np.float32).astype(np.float64)
+    q = g["q_xyzw"].astype(np.float32).astype(np.float64)
+    w = g["w"].astype(np.float32).astype(np.float64)
+    rew, reset = Q.compute_reward(p, tgt, q, w, None, g["progress"], int(g[f"{task}_max_ep"]), z_die)
+    np.testing.assert_allclose(rew, g[f"{task}_rew"], rtol=2e-6, atol=2e-6)
+    np.testing.assert_array_equal(reset, g[f"{task}_reset"])
