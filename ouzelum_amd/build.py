@@ -43,5 +43,21 @@ def build(force: bool = False, verbose: bool = True) -> str:
     return OUT
 
 
+EXAMPLE_SRC = os.path.join(ROOT, "examples", "c_host_step.cpp")
+EXAMPLE_OUT = os.path.join(ROOT, "examples", "c_host_step")
+
+
+def build_examples(verbose: bool = True) -> str:
+    """The C/C++ host example linked against the in-tree library (rpath to ouzelum_amd/)."""
+    cmd = [HIPCC, "-O2", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
+           "-I", os.path.join(ROOT, "include"), EXAMPLE_SRC, "-L", HERE, "-louzelum_hip",
+           "-Wl,-rpath,$ORIGIN/../ouzelum_amd", "-o", EXAMPLE_OUT]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return EXAMPLE_OUT
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    build_examples()

@@ -468,3 +468,20 @@ def test_ragged_sizes_parity(ouz, task, n):
         assert_close(f"{task}/{n}@{k} rew", g["rew"][ok], r["rew"][ok], 1e-5, 1e-5)
         np.testing.assert_array_equal(g["reset"][ok], r["reset"][ok])
         np.testing.assert_array_equal(g["progress"], r["progress"])
+
+
+def test_c_host_example_runs():
+    """examples/c_host_step.cpp drives the step through the C ABI with hipMalloc'd buffers only."""
+    import json
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "examples", "c_host_step")
+    if not os.path.exists(exe):
+        from ouzelum_amd import build
+        build.build_examples(verbose=False)
+    out = subprocess.run([exe, "4096", "300"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    assert d["step"] == 350 and d["obs0_finite"] == 1 and d["episodes"] >= 0
+    assert d["env_steps_per_s"] > 5e7                                # BASELINE target on one GPU
