@@ -28,6 +28,7 @@ namespace ouz {
 enum Ctrl { CTRL_RL = 0, CTRL_LEE_TRUE = 1, CTRL_LEE_EST = 2 };
 enum TargetMode { TGT_GOAL = 0, TGT_PLATFORM = 1, TGT_TRAJ = 2 };
 constexpr int kMixedChunk = 64;
+constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS staging is sized for it)
 
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
 struct TaskParams {
@@ -531,8 +532,32 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
-    pv_step(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u,
-            v3(vm[0], vm[1], vm[2]));
+    {
+      // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
+      // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
+      // LDS around it (lane-contiguous slots: conflict-free) so those registers are free at the peak
+      // (QuadTracking 270 -> fits 256: two waves per SIMD without scratch spills).
+      constexpr int kPark = 24;
+      __shared__ float s_park[kPark * kMaxBlock];
+      float* pk = s_park + threadIdx.x;
+      float vals[kPark] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
+                           S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
+                           S.dr_m, S.dr_i, S.dr_t};
+#pragma unroll
+      for (int k = 0; k < kPark; ++k) pk[k * kMaxBlock] = vals[k];
+      __asm__ volatile("" ::: "memory");   // no store-to-load forwarding: the registers die here
+      pv_step(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
+              g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
+      __asm__ volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < kPark; ++k) vals[k] = pk[k * kMaxBlock];
+      S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);
+      S.q = Q4{vals[9], vals[10], vals[11], vals[12]};
+      target = v3(vals[13], vals[14], vals[15]);
+      S.wp = v3(vals[16], vals[17], vals[18]);
+      S.plat = make_float2(vals[19], vals[20]);
+      S.dr_m = vals[21]; S.dr_i = vals[22]; S.dr_t = vals[23];
+    }
     S.prev_v = S.v;                                    // :454
     // waypoint guidance (:464-492)
     V3 wp = conv ? target : S.wp;
@@ -619,8 +644,6 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 // 3328-byte slice with 16-byte stores instead of 13 strided dword stores per lane.  Staging is
 // wave-local, so waves of one block may run different task paths (mixed curriculum).
 // ---------------------------------------------------------------------------
-constexpr int kMaxBlock = 256;
-
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
