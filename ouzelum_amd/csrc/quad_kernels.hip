@@ -811,17 +811,6 @@ __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, Rollou
   step_body<TASK, MULTI>(a, r);
 }
 
-// Large-N variant of the single-step kernel for the estimator tasks whose register peak sits just
-// above 256 (QuadTracking ~270, QuadMixed ~272): forcing 2 waves per SIMD costs ~15 spilled VGPRs
-// (scratch, L1/L2-resident) but overlaps two waves' HBM traffic.  Measured at 4 M / 16 M envs:
-// QuadTracking HBM fraction 0.51 -> 0.62, QuadMixed 0.32 -> 0.45; at 4096 envs (latency-bound, one
-// wave per CU) it is 2 % slower, so it is only launched above 65 536 envs.
-template <int TASK>
-__global__ void __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(2)))
-quad_step_kernel_occ2(StepArgs a, RolloutArgs r) {
-  step_body<TASK, false>(a, r);
-}
-
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
 __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1262,19 +1251,6 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
   return m;
 }
 
-extern "C++" {
-template <int T>
-static void launch_single(dim3 g, dim3 b, hipStream_t s, const StepArgs& a, const RolloutArgs& r, bool large) {
-  if constexpr (T == OUZ_TASK_TRACKING || T == OUZ_TASK_MIXED) {
-    if (large) {
-      hipLaunchKernelGGL(quad_step_kernel_occ2<T>, g, b, 0, s, a, r);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((quad_step_kernel<T, false>), g, b, 0, s, a, r);
-}
-}  // extern "C++"
-
 // Launch K (<= kMaxRolloutChunk) consecutive steps as ONE kernel.  K = 1 is VecTask.step.
 // ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
 // storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
@@ -1299,7 +1275,7 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
 #define OUZ_LAUNCH_TASK(T)                                         \
   do {                                                             \
     if (K == 1 && !storage) {                                      \
-      launch_single<T>(g, b, s, a, r, n > 65536);                  \
+      hipLaunchKernelGGL((quad_step_kernel<T, false>), g, b, 0, s, a, r); \
     } else {                                                       \
       auto kfn = quad_step_kernel<T, true>;                        \
       hipLaunchKernelGGL(kfn, g, b, 0, s, a, r);                   \

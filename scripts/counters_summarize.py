@@ -17,7 +17,7 @@ def main():
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    if "quad_step_kernel" in name and ("false>" in name or "occ2" in name) and row.get("Counter_Name") == c:
+                    if "quad_step_kernel" in name and "false>" in name and row.get("Counter_Name") == c:
                         vals.append(float(row["Counter_Value"]))
         res[c] = sum(vals) / len(vals) if vals else None
     if res.get("SQ_WAVES"):

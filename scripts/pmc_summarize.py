@@ -18,7 +18,7 @@ def avg_counter(path_glob, counter):
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
                 # the single-step launch (quad_step_kernel<TASK, false>), not the fused rollout variant
-                if "quad_step_kernel" in name and ("false>" in name or "occ2" in name) and row.get("Counter_Name") == counter:
+                if "quad_step_kernel" in name and "false>" in name and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 

@@ -429,9 +429,9 @@ def test_vectask_dr_noise_parity(ouz, obs_p, act_p):
 
 
 @pytest.mark.parametrize("task", ["QuadTracking", "QuadMixed"])
-def test_large_n_occupancy_variant_matches(ouz, task):
-    """Above 65 536 envs the estimator tasks launch the 2-waves-per-SIMD kernel variant; it runs the
-    same step body, so 70 016 envs in one env reproduce two 35 008-env shards bit for bit."""
+def test_large_n_matches_shards(ouz, task):
+    """Above 65 536 envs the step runs 256-lane blocks (4 waves sharing the LDS obs staging and the
+    parked PV-step state); 70 016 envs in one env reproduce two 35 008-env shards bit for bit."""
     from ouzelum_amd import _lib as L
     n = 70016
     full = ouz.make(seed=12, task=task, num_envs=n, sim_device="cuda:0", convergence_time=5)
