@@ -487,7 +487,11 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     float T;
     V3 tau;
     const V3 cmd = v3(0.0f, 0.0f, 1.0f);
+#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 1)
+    T = 0.5f + 0.01f * S.p.z; tau = S.w;
+#else
     lee_position(S.p, S.q, S.v, S.w, cmd, 0.0f, default_gains(), T, tau);
+#endif
     float fz = 2.0f * kGravity * T;
     V3 dd = cmd - S.p;
     if (sqrtf(dot(dd, dd)) < tp.land_radius) {
@@ -596,8 +600,12 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
     if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);
+#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 2)
+    S.p = S.p + 0.01f * S.v; S.v = S.v + inv_m * f_b; S.w = S.w + mul(tau_b, inv_I) + I;
+#else
     integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
               DeckContact{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y});
+#endif
   }
 
   // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
@@ -620,7 +628,11 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 #pragma unroll
   for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
+#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 4)
+  rew = p.x; dist = p.y;
+#else
   rew = reward(p, target, q, w, dist);
+#endif
   const bool timeout_len = S.progress >= tp.max_ep - 1;
   const bool die = dist > 8.0f || p.z < tp.z_die;
   rs = timeout_len || die;
