@@ -29,6 +29,9 @@ enum Ctrl { CTRL_RL = 0, CTRL_LEE_TRUE = 1, CTRL_LEE_EST = 2 };
 enum TargetMode { TGT_GOAL = 0, TGT_PLATFORM = 1, TGT_TRAJ = 2 };
 constexpr int kMixedChunk = 64;
 constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS staging is sized for it)
+// At or below this many envs a launch has at most 4 waves per CU and the step is latency-bound;
+// above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
+constexpr int kLatencyRegimeEnvs = 65536;
 
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
 struct TaskParams {
@@ -287,7 +290,11 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   S.w = ld3(S.T, OUZ_F_W);
   S.progress = ldi(S.T, OUZ_I_PROGRESS);
   S.dirty = 0;
-  S.land_flag = -1;
+  // The landing flag is only needed on reset.  In the latency regime (few waves per CU: the step is
+  // one dependent chain, load -> compute -> store) it is fetched with the state so the reset branch,
+  // taken by most waves once episodes desynchronise, does not wait on a second memory round trip.
+  // At large N that 4-byte load would be bandwidth; there the reset branch fetches it on demand.
+  S.land_flag = a.n <= kLatencyRegimeEnvs ? ldi(S.T, OUZ_I_LAND_FLAG) : -1;
   S.landings_add = 0;
   S.ep_cnt_add = 0;
   S.ep_len_add = 0;
@@ -331,13 +338,15 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
   sti(S.T, OUZ_I_PROGRESS, S.progress);
   if (a.track_episodes) {
     st(S.T, OUZ_F_EP_RET, S.ep_ret);
+    // accumulators: one lane owns each address, so a no-return atomic add is the same f32 / i32
+    // read-add-write without a load round trip before the wave can retire
     if (S.ep_cnt_add) {
-      st(S.T, OUZ_F_EP_SUM, ld(S.T, OUZ_F_EP_SUM) + S.ep_sum_add);
-      sti(S.T, OUZ_I_EP_CNT, ldi(S.T, OUZ_I_EP_CNT) + S.ep_cnt_add);
-      sti(S.T, OUZ_I_EP_LEN, ldi(S.T, OUZ_I_EP_LEN) + S.ep_len_add);
+      atomicAdd(&S.T.f[(uint32_t)OUZ_F_EP_SUM * 64u + S.T.l], S.ep_sum_add);
+      atomicAdd(&S.T.iv[(uint32_t)OUZ_I_EP_CNT * 64u + S.T.l], S.ep_cnt_add);
+      atomicAdd(&S.T.iv[(uint32_t)OUZ_I_EP_LEN * 64u + S.T.l], S.ep_len_add);
     }
   }
-  if (S.landings_add) sti(S.T, OUZ_I_LANDINGS, ldi(S.T, OUZ_I_LANDINGS) + S.landings_add);
+  if (S.landings_add) atomicAdd(&S.T.iv[(uint32_t)OUZ_I_LANDINGS * 64u + S.T.l], S.landings_add);
   if (S.dirty & D_LAND) sti(S.T, OUZ_I_LAND_FLAG, S.land_flag);
   if (S.dirty & D_DR) { st(S.T, OUZ_F_DR, S.dr_m); st(S.T, OUZ_F_DR + 1, S.dr_i); st(S.T, OUZ_F_DR + 2, S.dr_t); }
   if constexpr (TGT == TGT_GOAL) st3(S.T, OUZ_F_TARGET, S.target);
@@ -1064,7 +1073,7 @@ int hip_check(hipError_t e, const char* what) {
   return OUZ_OK;
 }
 inline int grid_for(int n, int block) { return (n + block - 1) / block; }
-inline int block_for(int n) { return n <= 65536 ? 64 : 256; }
+inline int block_for(int n) { return n <= kLatencyRegimeEnvs ? 64 : 256; }
 
 #define OUZ_LAUNCH_CHECK(what)                                         \
   do {                                                                 \
