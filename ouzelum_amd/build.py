@@ -21,7 +21,10 @@ FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wn
          "-fno-hip-fp32-correctly-rounded-divide-sqrt",
          # FMA contraction stays on everywhere except where a `#pragma clang fp contract(off)` asks for
          # torch's one-rounding-per-op order (RNG uniforms, GAE): __fmul_rn/__fadd_rn are plain operators in HIP.
-         "-ffp-contract=fast-honor-pragmas"]
+         "-ffp-contract=fast-honor-pragmas",
+         # no SLP packing of f32 pairs into v_pk_*: on this per-lane scalar code it only adds register-pair
+         # moves (v_mov -60 %, -5..7 % instructions per step phase) and ~40 VGPRs in the estimator kernels
+         "-fno-slp-vectorize"]
 
 
 def up_to_date() -> bool:

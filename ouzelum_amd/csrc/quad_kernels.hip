@@ -33,6 +33,31 @@ constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS stagin
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
 constexpr int kLatencyRegimeEnvs = 65536;
 
+// Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
+// single-step kernel, read back with ouz_probe_stamps.  Not part of the product library.
+#ifdef OUZ_PROBE_STAMPS
+constexpr int kStampSlots = 12, kStampWaves = 1024;
+__device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
+#define OUZ_STAMP(k, wait)                                                                       \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    if (wait) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                               \
+    const uint64_t _t = __builtin_amdgcn_s_memtime();                                            \
+    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                            \
+    if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+  } while (0)
+#define OUZ_STAMP_RT(k)                                                                          \
+  do {                                                                                           \
+    const uint64_t _t = __builtin_amdgcn_s_memrealtime();                                        \
+    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                            \
+    if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
+  } while (0)
+#else
+#define OUZ_STAMP(k, wait) do {} while (0)
+#define OUZ_STAMP_RT(k) do {} while (0)
+#endif
+
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
 struct TaskParams {
   int32_t ctrl, target_mode, max_ep, pomdp;
@@ -458,6 +483,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
   }
 
+  OUZ_STAMP(2, false);
   V3 f_b = v3(0.0f, 0.0f, 0.0f), tau_b = v3(0.0f, 0.0f, 0.0f);
 
   if constexpr (CTRL == CTRL_RL) {
@@ -603,6 +629,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     tau_b = tau;
   }
 
+  OUZ_STAMP(3, false);
   // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
   {
     const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
@@ -617,6 +644,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 #endif
   }
 
+  OUZ_STAMP(4, false);
   // ---- post_physics_step (ekf_lee_landed.py:620-685) ----
   S.progress += 1;
   if constexpr (TGT == TGT_GOAL) {
@@ -740,8 +768,11 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   const TaskParams& tp = a.tp[task];
   const uint32_t gid = a.env_offset + (uint32_t)i;
   EnvRegs<CTRL, TGT> S;
+  OUZ_STAMP_RT(8);
+  OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
   if (valid) env_load<CTRL, TGT>(a, i, tp, S);
+  OUZ_STAMP(1, true);
   if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
@@ -754,7 +785,9 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
     trace_count(a, ctx[0].step, did_reset, i);
 #endif
+    OUZ_STAMP(5, false);
     emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
+    OUZ_STAMP(6, false);
   } else {
     for (int k = 0; k < K; ++k) {
       float ob[OUZ_NUM_OBS];
@@ -779,6 +812,8 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     }
   }
   if (valid) env_store<CTRL, TGT>(a, i, tp, S);
+  OUZ_STAMP(7, true);
+  OUZ_STAMP_RT(9);
 }
 
 constexpr int kMaxRolloutChunk = 32;
@@ -1099,6 +1134,13 @@ struct ouz_env {
 };
 
 extern "C" {
+
+#ifdef OUZ_PROBE_STAMPS
+int ouz_probe_stamps(uint64_t* host, int32_t count) {
+  const int n = count < kStampWaves * kStampSlots ? count : kStampWaves * kStampSlots;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ouz_stamps), (size_t)n * sizeof(uint64_t)) == hipSuccess ? n : -1;
+}
+#endif
 
 int32_t ouz_abi_version(void) { return OUZ_ABI_VERSION; }
 const char* ouz_last_error(void) { return g_err.c_str(); }
