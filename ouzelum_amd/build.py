@@ -24,7 +24,11 @@ FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wn
          "-ffp-contract=fast-honor-pragmas",
          # no SLP packing of f32 pairs into v_pk_*: on this per-lane scalar code it only adds register-pair
          # moves (v_mov -60 %, -5..7 % instructions per step phase) and ~40 VGPRs in the estimator kernels
-         "-fno-slp-vectorize"]
+         "-fno-slp-vectorize",
+         # f32 denormals flush to zero: rcp / rsq / sqrt become single instructions instead of 5-6 with
+         # range scaling (-7..10 % instructions in the controller / integrator phases).  State, RNG uniforms
+         # and learner tensors are normal floats; f64 (the PV filter) keeps denormals.
+         "-fgpu-flush-denormals-to-zero"]
 
 
 def up_to_date() -> bool:

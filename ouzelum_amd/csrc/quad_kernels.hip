@@ -639,7 +639,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 #if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 2)
     S.p = S.p + 0.01f * S.v; S.v = S.v + inv_m * f_b; S.w = S.w + mul(tau_b, inv_I) + I;
 #else
-    integrate(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
+    integrate<true>(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
               DeckContact{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y});
 #endif
   }

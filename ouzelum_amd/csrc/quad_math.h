@@ -589,12 +589,15 @@ struct DeckContact {
   float px, py, vx, vy;   // platform position / velocity (xy)
 };
 
+// kThrustOnly: f_b = (0, 0, f_b.z) (every task's rotor force is along body z); the world force is then
+// R's third column times f_b.z, the same value mv(R, f_b) rounds to without its multiplies by zero.
+template <bool kThrustOnly = false>
 OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m, V3 I, V3 inv_I, float dt,
                       int substeps, float wmax, DeckContact deck = DeckContact{false, 0.f, 0.f, 0.f, 0.f}) {
   const float h = dt / (float)substeps;
   for (int s = 0; s < substeps; ++s) {
     M3 R = quat_to_mat(q);
-    V3 fw = mv(R, f_b);
+    V3 fw = kThrustOnly ? v3(R.m[2] * f_b.z, R.m[5] * f_b.z, R.m[8] * f_b.z) : mv(R, f_b);
     v = v + h * v3(fw.x * inv_m, fw.y * inv_m, fw.z * inv_m - kGravity);
     V3 wb = mtv(R, w);
     V3 c = cross(wb, mul(I, wb));
