@@ -13,7 +13,8 @@ import os
 import torch  # noqa: F401  -- load torch's HIP runtime first so ours binds to the same libamdhip64
 
 LIB_NAME = "libouzelum_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# OUZ_LIB: an alternative in-tree build (probe builds of scripts/; never the product default)
+LIB_PATH = os.environ.get("OUZ_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
 
 class OuzelumError(RuntimeError):

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, "csrc", "quad_kernels.hip"), os.path.join(HERE, "csrc", "learner_kernels.hip")]
 DEPS = [*SRCS, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc", "philox.h"),
         os.path.join(ROOT, "include", "ouzelum.h")]
-OUT = os.path.join(HERE, "libouzelum_hip.so")
+OUT = os.environ.get("OUZ_BUILD_OUT") or os.path.join(HERE, "libouzelum_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OUZ_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",

@@ -43,14 +43,14 @@ __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
     __builtin_amdgcn_sched_barrier(0);                                                           \
     if (wait) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                               \
     const uint64_t _t = __builtin_amdgcn_s_memtime();                                            \
-    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                            \
+    const uint32_t _w = (uint32_t)i >> 6;   /* env index of the enclosing function */              \
     if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
     __builtin_amdgcn_sched_barrier(0);                                                           \
   } while (0)
 #define OUZ_STAMP_RT(k)                                                                          \
   do {                                                                                           \
     const uint64_t _t = __builtin_amdgcn_s_memrealtime();                                        \
-    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                            \
+    const uint32_t _w = (uint32_t)i >> 6;   /* env index of the enclosing function */              \
     if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
   } while (0)
 #else
@@ -116,8 +116,15 @@ struct StepArgs {
   uint32_t* trace_resets;      // [trace_cap] envs reset at the start of each step
   int32_t trace_env, trace_cap;
   EnvConsts c;
-  TaskParams tp[OUZ_NUM_TASKS];
+  TaskParams tp[3];            // by tp_slot(task): the configured task, or the three curriculum tasks
 };
+
+// Task-parameter slot: a single-task env fills only its task's slot, the mixed curriculum the slots of
+// LeeLanded (0), QuadTracking (1) and QuadFault (2).  Three slots instead of one per task keep the
+// kernel arguments (copied by the host on every launch) at 168 instead of 336 bytes of parameters.
+__host__ __device__ constexpr int tp_slot(int task) {
+  return task == OUZ_TASK_TRACKING ? 1 : (task == OUZ_TASK_FAULT ? 2 : 0);
+}
 
 // x500 lumped body (assets/x500/x500.urdf).  Rotor arms, x500.urdf:3-29.
 __device__ __constant__ float kRotorX[4] = {0.174f, -0.174f, 0.174f, -0.174f};
@@ -307,8 +314,13 @@ struct EnvRegs {
 
 template <int CTRL, int TGT>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S) {
-  S.rst = (a.reset + S.T.first)[S.T.l] != 0;
-  S.flags_clear = !S.rst && (a.timeouts + S.T.first)[S.T.l] == 0;   // issued with the state loads
+  // reset_buf and time_outs are read unconditionally and combined without a branch, so the two flag
+  // loads and the state loads below are in flight together (one memory round trip, not three:
+  // a short-circuit `!rst && timeouts == 0` made the time-out load wait for the reset load).
+  const int64_t rv = (a.reset + S.T.first)[S.T.l];
+  const uint32_t tv = (a.timeouts + S.T.first)[S.T.l];
+  S.rst = rv != 0;
+  S.flags_clear = (rv == 0) & (tv == 0u);
   S.p = ld3(S.T, OUZ_F_P);
   S.q = Q4{ld(S.T, OUZ_F_Q), ld(S.T, OUZ_F_Q + 1), ld(S.T, OUZ_F_Q + 2), ld(S.T, OUZ_F_Q + 3)};
   S.v = ld3(S.T, OUZ_F_V);
@@ -445,7 +457,7 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
 template <int CTRL, int TGT>
 __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
                                          EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout) {
-  const TaskParams& tp = a.tp[task];
+  const TaskParams& tp = a.tp[tp_slot(task)];
   const EnvConsts& c = a.c;
   const bool rst = S.rst;
   // target_root_positions: random goals are state (ouzelum.py:180-190); a platform target is
@@ -765,7 +777,7 @@ template <int CTRL, int TGT, bool MULTI>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, bool valid, int task,
                                         bool direct = false) {
-  const TaskParams& tp = a.tp[task];
+  const TaskParams& tp = a.tp[tp_slot(task)];
   const uint32_t gid = a.env_offset + (uint32_t)i;
   EnvRegs<CTRL, TGT> S;
   OUZ_STAMP_RT(8);
@@ -825,23 +837,48 @@ struct RolloutArgs {
   StepCtx ctx[kMaxRolloutChunk];
 };
 
+// Launch block size, a function of n only (the host launches with the same rule): the kernel
+// derives it from a.n instead of reading blockDim from the hidden kernel arguments, whose cache
+// line would be one more scalar-memory miss at entry.
+__host__ __device__ __forceinline__ int step_block_for(int n) { return n <= kLatencyRegimeEnvs ? 64 : 256; }
+
+// Kernel-argument prefetch.  The step kernel reads its ~1 KB argument block through scalar loads
+// that the compiler issues in several dependent batches (each waits for the previous: SGPR reuse,
+// branches on loaded values), and in the latency regime every batch is a scalar-cache miss on a
+// freshly written argument buffer.  One dword per 64-byte line, all issued together and waited for
+// once, turns those serial misses into one; the later field loads hit the scalar cache.
+// (All sixteen dwords are operands of one asm statement, so the compiler must have issued every
+// load before it and waits once; folding them into one value let it wait after every eight.)
+template <int NBYTES>
+__device__ __forceinline__ void prefetch_kernargs() {
+  const __attribute__((address_space(4))) uint32_t* kp =
+      (const __attribute__((address_space(4))) uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  constexpr int kLines = (NBYTES + 63) / 64 < 16 ? (NBYTES + 63) / 64 : 16;
+  uint32_t t[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) t[k] = kp[(k < kLines ? k : kLines - 1) * 16];
+  __asm__ volatile("" ::"s"(t[0]), "s"(t[1]), "s"(t[2]), "s"(t[3]), "s"(t[4]), "s"(t[5]), "s"(t[6]), "s"(t[7]),
+                   "s"(t[8]), "s"(t[9]), "s"(t[10]), "s"(t[11]), "s"(t[12]), "s"(t[13]), "s"(t[14]), "s"(t[15]));
+}
+
 // The step kernel body: one env per lane, K steps (MULTI) or one.
 template <int TASK, bool MULTI>
-__device__ __forceinline__ void step_body(const StepArgs& a, const RolloutArgs& r) {
+__device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
+                                          uint64_t out_stride) {
   __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;
   const int first = i - (int)(threadIdx.x & 63);
   if (first >= a.n) return;                 // whole wave past the end
   const bool valid = i < a.n;
   if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-    run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_RL, TGT_GOAL, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
   } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
   } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -851,20 +888,32 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const RolloutArgs& 
     const bool vl = valid && t == OUZ_TASK_LEE_LANDED, vt = valid && t == OUZ_TASK_TRACKING;
     const bool vr = valid && !vl && !vt;
     if (__any(vl))
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vl,
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vl,
                                                   OUZ_TASK_LEE_LANDED, direct);
     if (__any(vt))
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vt,
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vt,
                                              OUZ_TASK_TRACKING, direct);
     if (__any(vr))
-      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, r.ctx, r.K, r.outs, r.out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
+      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
                                         direct);
   }
 }
 
-template <int TASK, bool MULTI>
-__global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, RolloutArgs r) {
-  step_body<TASK, MULTI>(a, r);
+// VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
+// (~390 B): the host copies the argument block on every launch (≈0.6 us more host time per launch
+// for a 1.1 KB block, scripts/exp/launch_cost.hip), and at 4096 envs that host time is the bound.
+template <int TASK>
+__global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCtx c) {
+  prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
+  const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
+  step_body<TASK, false>(a, &c, 1, env_out, 0);
+}
+
+// ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.
+template <int TASK>
+__global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
+  prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
+  step_body<TASK, true>(a, r.ctx, r.K, r.outs, r.out_stride);
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
@@ -873,7 +922,7 @@ __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   if (i >= a.n) return;
   const uint32_t gid = a.env_offset + (uint32_t)i;
   const int task = task_cfg == OUZ_TASK_MIXED ? mixed_task(gid) : task_cfg;
-  const TaskParams& tp = a.tp[task];
+  const TaskParams& tp = a.tp[tp_slot(task)];
   for (int k = 0; k < OUZ_F_COUNT; ++k) st(a, k, i, 0.0f);
   for (int k = 0; k < OUZ_I_COUNT; ++k) sti(a, k, i, 0);
   st(a, OUZ_F_P + 2, i, 1.0f);           // default_pose.p.z = 1 (ekf_lee_landed.py:228-229)
@@ -1108,7 +1157,7 @@ int hip_check(hipError_t e, const char* what) {
   return OUZ_OK;
 }
 inline int grid_for(int n, int block) { return (n + block - 1) / block; }
-inline int block_for(int n) { return n <= kLatencyRegimeEnvs ? 64 : 256; }
+inline int block_for(int n) { return step_block_for(n); }   // the step kernel assumes this rule
 
 #define OUZ_LAUNCH_CHECK(what)                                         \
   do {                                                                 \
@@ -1249,6 +1298,10 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
                   cfg->substeps, cfg->convergence_time, (float)mass, (float)ixx, (float)ixx, (float)izz,
                   1.0f / (float)mass, 1.0f / (float)ixx, 1.0f / (float)ixx, 1.0f / (float)izz};
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
+    const bool used = cfg->task == OUZ_TASK_MIXED
+                          ? (t == OUZ_TASK_LEE_LANDED || t == OUZ_TASK_TRACKING || t == OUZ_TASK_FAULT)
+                          : t == cfg->task;
+    if (!used) continue;
     TaskParams tp = task_preset(t);
     if (cfg->pomdp >= 0) tp.pomdp = cfg->pomdp;
     if (cfg->pomdp_prob >= 0.0f) tp.pomdp_prob = cfg->pomdp_prob;
@@ -1256,7 +1309,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     double prob = (double)tp.pomdp_prob;
     tp.noise_lo = (float)(1.0 - prob);
     tp.noise_hi = (float)(1.0 + prob);
-    a.tp[t] = tp;
+    a.tp[tp_slot(t)] = tp;
   }
   *out = e;
   return OUZ_OK;
@@ -1302,8 +1355,10 @@ int ouz_init_state(ouz_env* env, void* stream) {
 static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
   uint32_t m = 0;
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
-    if (cfg_task != OUZ_TASK_MIXED && t != cfg_task) continue;
-    const TaskParams& tp = a.tp[t];
+    if (cfg_task != OUZ_TASK_MIXED ? t != cfg_task
+                                   : !(t == OUZ_TASK_LEE_LANDED || t == OUZ_TASK_TRACKING || t == OUZ_TASK_FAULT))
+      continue;
+    const TaskParams& tp = a.tp[tp_slot(t)];
     if (tp.pomdp != OUZ_POMDP_FLICKER && tp.pomdp != OUZ_POMDP_FLICKER_NOISE) continue;
     const float p = tp.pomdp == OUZ_POMDP_FLICKER ? tp.pomdp_prob : 0.1f;
     for (uint32_t site = 0; site < 6; ++site) {
@@ -1338,10 +1393,9 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
 #define OUZ_LAUNCH_TASK(T)                                         \
   do {                                                             \
     if (K == 1 && !storage) {                                      \
-      hipLaunchKernelGGL((quad_step_kernel<T, false>), g, b, 0, s, a, r); \
+      hipLaunchKernelGGL(quad_step_kernel<T>, g, b, 0, s, a, r.ctx[0]); \
     } else {                                                       \
-      auto kfn = quad_step_kernel<T, true>;                        \
-      hipLaunchKernelGGL(kfn, g, b, 0, s, a, r);                   \
+      hipLaunchKernelGGL(quad_rollout_kernel<T>, g, b, 0, s, a, r); \
     }                                                              \
   } while (0)
   switch (env->cfg.task) {

@@ -1,4 +1,4 @@
-"""Average per-dispatch value of PMC counters of the single-step kernel (quad_step_kernel<T, false>).
+"""Average per-dispatch value of PMC counters of the single-step kernel (quad_step_kernel<T>; the fused rollout is quad_rollout_kernel<T>).
 python counters_summarize.py OUTDIR TAG TASK N COUNTER...  -> OUTDIR/cnt_TAG_TASK_N_summary.json"""
 import csv
 import glob
@@ -17,7 +17,7 @@ def main():
             with open(f) as fh:
                 for row in csv.DictReader(fh):
                     name = row.get("Kernel_Name", "")
-                    if "quad_step_kernel" in name and "false>" in name and row.get("Counter_Name") == c:
+                    if "quad_step_kernel<" in name and row.get("Counter_Name") == c:
                         vals.append(float(row["Counter_Value"]))
         res[c] = sum(vals) / len(vals) if vals else None
     if res.get("SQ_WAVES"):

@@ -17,8 +17,8 @@ def avg_counter(path_glob, counter):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
-                # the single-step launch (quad_step_kernel<TASK, false>), not the fused rollout variant
-                if "quad_step_kernel" in name and "false>" in name and row.get("Counter_Name") == counter:
+                # the single-step launch (quad_step_kernel<TASK>), not quad_rollout_kernel<TASK>
+                if "quad_step_kernel<" in name and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
