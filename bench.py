@@ -152,7 +152,7 @@ def cpu_baseline(task, n, seed, budget_s):
 
 def main():
     args = parse()
-    from ouzelum_amd.distributed import allreduce_returns, init_from_env, shard
+    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env, shard
     rank, world, local = init_from_env()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
@@ -166,6 +166,11 @@ def main():
     storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
                torch.empty((RING, n), dtype=torch.int64, device=dev), torch.empty((RING, n), dtype=torch.bool, device=dev))
 
+    # per-rollout return all-reduce (RCCL when N > 1), asynchronous on the collective's stream and
+    # double-buffered so the next rollout's steps do not wait for it (distributed.ReturnAllReduce)
+    red = ReturnAllReduce(dev)
+    n_roll = [0]
+
     def rollouts(steps, fused=False):
         done = 0
         while done < steps:
@@ -174,10 +179,11 @@ def main():
                 env.rollout(ring, k, fused=True, storage=tuple(t[:k] for t in storage))
             else:       # one kernel launch per VecTask.step
                 env.rollout(ring, k)
-            stats = env.episode_stats()
-            if world > 1:
-                dist.all_reduce(stats)
+            env.episode_stats(out=red.slot(n_roll[0]))
+            red.submit(n_roll[0])
+            n_roll[0] += 1
             done += k
+        red.finish()
 
     def timed(steps, fused=False):
         torch.cuda.synchronize(dev)
@@ -229,7 +235,7 @@ def main():
         "config": {"workload": f"config B: {n}-env x500 hover, Lee position controller ({args.task}), fp32, "
                                "dt 0.01 x 2 sub-steps",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
-                   "parallelism": f"env-sharded dp{world} (RCCL return all-reduce per 16-step rollout)"},
+                   "parallelism": f"env-sharded dp{world} (async RCCL return all-reduce per 16-step rollout)"},
         "roofline": roofline_entry(args.task, n, us),
         "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
     }

@@ -497,6 +497,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 
   OUZ_STAMP(2, false);
   V3 f_b = v3(0.0f, 0.0f, 0.0f), tau_b = v3(0.0f, 0.0f, 0.0f);
+  M3 R0;   // quat_to_mat of the (post-reset) state quaternion: shared by the controller and the integrator
 
   if constexpr (CTRL == CTRL_RL) {
     // ---- RL per-rotor thrust model (ouzelum.py:218-251) ----
@@ -534,10 +535,11 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     float T;
     V3 tau;
     const V3 cmd = v3(0.0f, 0.0f, 1.0f);
+    R0 = quat_to_mat(S.q);
 #if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 1)
     T = 0.5f + 0.01f * S.p.z; tau = S.w;
 #else
-    lee_position(S.p, S.q, S.v, S.w, cmd, 0.0f, default_gains(), T, tau);
+    lee_position_R(R0, S.p, S.v, S.w, cmd, 0.0f, default_gains(), T, tau);
 #endif
     float fz = 2.0f * kGravity * T;
     V3 dd = cmd - S.p;
@@ -627,8 +629,9 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     S.wp = wp;
     float T;
     V3 tau;
-    if (conv) lee_position(S.p, S.q, S.v, S.w, wp, 0.0f, default_gains(), T, tau);
-    else lee_position(v3(S.px[0], S.px[1], S.px[2]), S.q, v3(S.px[3], S.px[4], S.px[5]), S.w, wp, 0.0f, default_gains(), T, tau);
+    R0 = quat_to_mat(S.q);   // after the PV step's register peak
+    if (conv) lee_position_R(R0, S.p, S.v, S.w, wp, 0.0f, default_gains(), T, tau);
+    else lee_position_R(R0, v3(S.px[0], S.px[1], S.px[2]), v3(S.px[3], S.px[4], S.px[5]), S.w, wp, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
     if (td < tp.land_radius) {                       // :508-515
       if (!conv) { S.land_flag = 1; S.dirty |= D_LAND; }
@@ -651,8 +654,13 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 #if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 2)
     S.p = S.p + 0.01f * S.v; S.v = S.v + inv_m * f_b; S.w = S.w + mul(tau_b, inv_I) + I;
 #else
-    integrate<true>(S.p, S.q, S.v, S.w, f_b, tau_b, inv_m, I, inv_I, c.dt, c.substeps, c.wmax,
-              DeckContact{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y});
+    if constexpr (CTRL == CTRL_RL) R0 = quat_to_mat(S.q);
+    const DeckContact deck{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y};
+    const float h = c.dt / (float)c.substeps;
+    if (c.substeps == 2)   // the configured sub-step count (EKFLeeLanded.yaml:29), unrolled
+      integrate_thrust_body<2>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck);
+    else
+      integrate_thrust_body<0>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck, c.substeps);
 #endif
   }
 

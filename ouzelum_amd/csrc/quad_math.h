@@ -212,9 +212,9 @@ OUZ_HD V3 lee_attitude_loop(const M3& R, const M3& Rd, V3 omega, const EulerSC& 
 
 // LeePositionController.__call__ (controllers/position_control.py:19-109).
 // cmd = (x, y, z, yaw); thrust in units of m*g, torque "inertia normalised".
-OUZ_HD void lee_position(V3 p, Q4 q, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const LeeGains& g, float& thrust,
-                         V3& torque) {
-  M3 R = quat_to_mat(q);
+// R = quat_to_mat(q) of the state quaternion (the step kernel shares it with the integrator).
+OUZ_HD void lee_position_R(const M3& R, V3 p, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const LeeGains& g,
+                           float& thrust, V3& torque) {
   EulerSC e = euler_sc(R);
   V3 a = mul(g.kP, cmd_p - p) - mul(g.kV, v);
   a.z += 1.0f;
@@ -227,6 +227,11 @@ OUZ_HD void lee_position(V3 p, Q4 q, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const 
   float yr = remainder_f(cmd_yaw - atan2f(R.m[3], R.m[0]), kTwoPiF);
   if (yr > kPiF) yr -= kTwoPiF;
   torque = lee_attitude_loop(R, Rd, w, e, yr, g);
+}
+
+OUZ_HD void lee_position(V3 p, Q4 q, V3 v, V3 w, V3 cmd_p, float cmd_yaw, const LeeGains& g, float& thrust,
+                         V3& torque) {
+  lee_position_R(quat_to_mat(q), p, v, w, cmd_p, cmd_yaw, g, thrust, torque);
 }
 
 // LeeVelocityController.__call__ (controllers/velocity_control.py:17-112).
@@ -632,6 +637,56 @@ OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m,
     float qi = 1.0f / sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
     q = Q4{q.x * qi, q.y * qi, q.z * qi, q.w * qi};
   }
+}
+
+// The same integrator specialised for the fused step (every task's body force is a thrust along
+// body z) with the angular velocity carried in the body frame across sub-steps.  The attitude
+// increment of a sub-step rotates about w itself (dq = exp(w h / 2) ⊗ q), so R_{s+1}^T w = R_s^T w:
+// the body rate after sub-step s is the next sub-step's input without the world -> body -> world
+// round trip, and dq ⊗ q = q ⊗ exp(w_b h / 2).  Algebraically identical to integrate<true>
+// (the oracle keeps the world-frame form); it needs R(q) once at entry (shared with the
+// controller), R(q)'s third column between sub-steps and R(q) once at exit for the world-frame w.
+// |w| = |w_b| (the clamp) and w = 0 <=> w_b = 0 (the deck) carry over unchanged.
+// NSUB > 0: that many sub-steps, unrolled; NSUB = 0: nsub sub-steps in a loop.
+template <int NSUB>
+OUZ_HD void integrate_thrust_body(V3& p, Q4& q, V3& v, V3& w, const M3& R0, float fz, V3 tau_b, float inv_m, V3 I,
+                                  V3 inv_I, float h, float wmax, DeckContact deck, int nsub = NSUB) {
+  V3 wb = mtv(R0, w);
+  V3 z = v3(R0.m[2], R0.m[5], R0.m[8]);
+  const float acc = fz * inv_m;
+  for (int s = 0; s < (NSUB > 0 ? NSUB : nsub); ++s) {   // a constant NSUB unrolls by itself
+    if (s > 0)   // third column of R(q) for the unit quaternion q (normalised at the end of every sub-step)
+      z = v3(2.0f * (q.x * q.z + q.y * q.w), 2.0f * (q.y * q.z - q.x * q.w), 1.0f - 2.0f * (q.x * q.x + q.y * q.y));
+    v = v + h * v3(z.x * acc, z.y * acc, z.z * acc - kGravity);
+    const V3 c = cross(wb, mul(I, wb));
+    wb = wb + h * mul(inv_I, tau_b - c);
+    float n2 = dot(wb, wb);
+    if (n2 > wmax * wmax) { wb = (wmax / sqrtf(n2)) * wb; n2 = wmax * wmax; }
+    p = p + h * v;
+    if (deck.on) {
+      const float dx = p.x - deck.px, dy = p.y - deck.py;
+      if (dx * dx + dy * dy < kDeckRadius2 && p.z < kDeckZRest) {
+        p.z = kDeckZRest;
+        v = v3(deck.vx, deck.vy, fmaxf(v.z, 0.0f));
+        wb = v3(0.0f, 0.0f, 0.0f);
+        n2 = 0.0f;
+      }
+    }
+    const float n = sqrtf(n2);
+    const float th = 0.5f * h * n, th2 = th * th;
+    float sc, co;
+    if (th < 0.1f) {
+      sc = 0.5f * h * (1.0f - th2 * (1.0f / 6.0f) * (1.0f - th2 * (1.0f / 20.0f)));
+      co = 1.0f - 0.5f * th2 * (1.0f - th2 * (1.0f / 12.0f) * (1.0f - th2 * (1.0f / 30.0f)));
+    } else {
+      sc = sinf(th) / n;
+      co = cosf(th);
+    }
+    q = quat_mul(q, Q4{wb.x * sc, wb.y * sc, wb.z * sc, co});
+    const float qi = 1.0f / sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q = Q4{q.x * qi, q.y * qi, q.z * qi, q.w * qi};
+  }
+  w = mv(quat_to_mat(q), wb);
 }
 
 }  // namespace ouz

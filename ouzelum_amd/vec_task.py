@@ -217,17 +217,23 @@ class QuadVecTask:
         """Total landings over all finished episodes (ekf_lee_landed.py:319-331 'Landoa')."""
         return int(self.istate[:, L.I_LANDINGS].sum().item())
 
-    def episode_stats(self, drain=True):
+    def episode_stats(self, drain=True, out=None):
         """[sum of returns, count, sum of lengths] of episodes finished since the last drain, as a
         float64 device tensor — the quantities RecordEpisodeStatisticsTorch reports as info["r"] /
         info["l"] (PPO/utils.py:20-35); config E all-reduces it over RCCL.  One kernel
-        (``ouz_episode_stats``).  The tensor is returned by reference and overwritten by the next
-        call, like ``rew_buf``; clone it to keep it.  Needs ``track_episodes=True``."""
+        (``ouz_episode_stats``).  Without ``out`` the tensor is returned by reference and overwritten
+        by the next call, like ``rew_buf``; ``out`` (a contiguous float64 tensor of 3 on this device)
+        receives it instead, e.g. a slot of a ring while an asynchronous all-reduce of the previous
+        slot is still in flight.  Needs ``track_episodes=True``."""
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
-        L.check(L.lib.ouz_episode_stats(self._env, L.ptr(self._stats_buf), 1 if drain else 0, self._stream()),
+        buf = self._stats_buf if out is None else out
+        if out is not None and (out.dtype != torch.float64 or out.numel() < 3 or not out.is_contiguous()
+                                or out.device != self.device):
+            raise ValueError("episode_stats: out must be a contiguous float64 tensor of >= 3 on the env device")
+        L.check(L.lib.ouz_episode_stats(self._env, L.ptr(buf), 1 if drain else 0, self._stream()),
                 "ouz_episode_stats")
-        return self._stats_buf
+        return buf
 
     _DRN_DIST = {"gaussian": 1, "uniform": 2}
     _DRN_OP = {"additive": 0, "scaling": 1}

@@ -129,3 +129,33 @@ def test_learner_data_parallel_gradients(tmp_path):
     for a, b, p in zip(g0, g1, net.parameters()):
         assert torch.equal(a, b)
         torch.testing.assert_close(a, p.grad, rtol=1e-5, atol=1e-7)
+
+
+def _async_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env
+    init_from_env(backend="gloo")
+    red = ReturnAllReduce(torch.device("cpu"), depth=2)
+    assert red.active
+    got = []
+    for r in range(7):   # bench.py's pattern: fill slot r % 2, submit, keep stepping; read back later
+        red.slot(r).copy_(torch.tensor([10.0 * r + rank, 1.0 + rank, float(r)], dtype=torch.float64))
+        red.submit(r)
+        if r >= 1:
+            got.append(red.result(r - 1).clone())
+    got.append(red.result(6).clone())
+    red.finish()
+    torch.save(torch.stack(got), os.path.join(out_dir, f"a{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_return_allreduce(tmp_path):
+    """ReturnAllReduce (the double-buffered asynchronous per-rollout all-reduce of bench.py) gives every
+    rank the global [sum, count, ...] of each rollout, and a slot is not overwritten while in flight."""
+    mp.spawn(_async_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    a0 = torch.load(tmp_path / "a0.pt", weights_only=True)
+    a1 = torch.load(tmp_path / "a1.pt", weights_only=True)
+    want = torch.tensor([[20.0 * r + 1, 3.0, 2.0 * r] for r in range(7)], dtype=torch.float64)
+    assert torch.equal(a0, want) and torch.equal(a1, want)
