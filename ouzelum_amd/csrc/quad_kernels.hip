@@ -298,6 +298,7 @@ struct EnvRegs {
   bool flags_clear;               // reset_buf == 0 and time_outs == 0 in the buffers (emit may skip them)
   V3 target;                      // TGT_GOAL: stored random goal
   float thrust[4];                // CTRL_RL
+  float4 act;                     // CTRL_RL: this step's action row, loaded with the state
   int32_t frot, fonset;           // fault
   float eta;
   float dr_m, dr_i, dr_t;         // domain randomisation scales
@@ -306,14 +307,24 @@ struct EnvRegs {
   float eP[10], px[9], pP[45];
   float2 plat;                    // platform xy (TGT_TRAJ state; (0, 0) for TGT_PLATFORM)
   float2 plat_v;                  // this step's platform velocity (deck contact)
+  int32_t ttype, tidx;            // TGT_TRAJ: trajectory type and waypoint index, scale * direction and
+  float tsd, heading;             //   the husky's heading (landing.py:208-213), loaded with the state
+  float2 wp_cur, wp_next;         //   waypoints tidx and tidx + 1, fetched at the start of the step
   int32_t land_flag;              // -1: not loaded (only needed on reset / landing)
   int32_t landings_add, ep_cnt_add, ep_len_add;
   float ep_ret, ep_sum_add;
   uint32_t dirty;
 };
 
+// One env's action row (vec_task.py:313: actions (N, 4) f32 on rl_device): a 16-byte load per lane.
 template <int CTRL, int TGT>
-__device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S) {
+__device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL, TGT>& S) {
+  if constexpr (CTRL == CTRL_RL) S.act = reinterpret_cast<const float4*>(actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
+}
+
+template <int CTRL, int TGT>
+__device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S,
+                                         const float* actions) {
   // reset_buf and time_outs are read unconditionally and combined without a branch, so the two flag
   // loads and the state loads below are in flight together (one memory round trip, not three:
   // a short-circuit `!rst && timeouts == 0` made the time-out load wait for the reset load).
@@ -345,6 +356,9 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
     for (int k = 0; k < 4; ++k) S.thrust[k] = ld(S.T, OUZ_F_THRUST + k);
     S.frot = -1; S.fonset = 0; S.eta = 1.0f;
     if (tp.fault) { S.frot = ldi(S.T, OUZ_I_FAULT_ROTOR); S.fonset = ldi(S.T, OUZ_I_FAULT_ONSET); S.eta = ld(S.T, OUZ_F_FAULT_ETA); }
+    // in flight with the state loads: issued inside the step it would be a second memory round trip
+    // behind the reset branch (every wave's critical path, and half the bytes in flight at large N)
+    load_actions<CTRL, TGT>(actions, S);
   }
   if constexpr (CTRL == CTRL_LEE_EST) {
     S.prev_v = ld3(S.T, OUZ_F_PREV_V);
@@ -359,6 +373,8 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   }
   if constexpr (TGT == TGT_TRAJ) {
     S.plat = make_float2(ld(S.T, OUZ_F_PLAT), ld(S.T, OUZ_F_PLAT + 1));
+    S.ttype = ldi(S.T, OUZ_I_TRAJ_TYPE); S.tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
+    S.tsd = ld(S.T, OUZ_F_TRAJ_SD); S.heading = ld(S.T, OUZ_F_PLAT_HEADING);
 
   } else {
     S.plat = make_float2(0.0f, 0.0f);
@@ -405,36 +421,46 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
   }
   if constexpr (TGT == TGT_TRAJ) {
     st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y);
+    sti(S.T, OUZ_I_TRAJ_IDX, S.tidx); st(S.T, OUZ_F_PLAT_HEADING, S.heading);
+    if (S.dirty & D_TRAJ) { sti(S.T, OUZ_I_TRAJ_TYPE, S.ttype); st(S.T, OUZ_F_TRAJ_SD, S.tsd); }
+  }
+}
+
+// Waypoints tidx and tidx + 1 of the env's trajectory (table reads), issued at the start of the step
+// so that their latency hides behind the estimator; platform_step picks one of them.
+template <int CTRL, int TGT>
+__device__ __forceinline__ void platform_prefetch(const StepArgs& a, EnvRegs<CTRL, TGT>& S) {
+  if constexpr (TGT == TGT_TRAJ) {
+    S.wp_cur = traj_point(a, S.ttype, S.tidx, S.tsd);
+    S.wp_next = traj_point(a, S.ttype, S.tidx + 1, S.tsd);   // clamped to the last waypoint
   }
 }
 
 // The husky following its waypoints (landing.py:319-364) as a kinematic differential-drive unicycle
 // (oracle OracleEnv._platform_step).  Runs right before the integrator: nothing earlier in the step
-// reads the platform (the target comes from the previous step's position), so the trajectory state
-// (type, index, scale, heading) is loaded, advanced and stored here and never held across the
-// estimator's register peak.
+// reads the platform (the target comes from the previous step's position).  The trajectory state is
+// loaded with the env state and the two candidate waypoints at the start of the step, so the only
+// memory access left here is the first waypoint of a freshly drawn trajectory.
 template <int CTRL, int TGT>
 __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& sc, uint32_t gid,
                                               EnvRegs<CTRL, TGT>& S) {
   const EnvConsts& c = a.c;
-  int ttype = ldi(S.T, OUZ_I_TRAJ_TYPE), tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
-  float sd = ld(S.T, OUZ_F_TRAJ_SD), th = ld(S.T, OUZ_F_PLAT_HEADING);
-  float2 wpp = traj_point(a, ttype, tidx, sd);
+  float2 wpp = S.wp_cur;
   float dx = wpp.x - S.plat.x, dy = wpp.y - S.plat.y;
-  if (sqrtf(dx * dx + dy * dy) < 0.2f) tidx += 1;
-  const int len = ttype == 0 ? kTrajLen[0] : (ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
-  if (tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
+  if (sqrtf(dx * dx + dy * dy) < 0.2f) { S.tidx += 1; wpp = S.wp_next; }
+  const int len = S.ttype == 0 ? kTrajLen[0] : (S.ttype == 1 ? kTrajLen[1] : kTrajLen[2]);
+  if (S.tidx >= len) {   // reset_completed_trajectories (landing.py:215-235)
     U4 r = draw(a.seed, gid, sc.step, RNG_TRAJ);
-    ttype = (int)(r.x % 3u);
-    sd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
-    tidx = 0;
-    sti(S.T, OUZ_I_TRAJ_TYPE, ttype);
-    st(S.T, OUZ_F_TRAJ_SD, sd);
+    S.ttype = (int)(r.x % 3u);
+    S.tsd = (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f);
+    S.tidx = 0;
+    S.dirty |= D_TRAJ;
+    wpp = traj_point(a, S.ttype, 0, S.tsd);
   }
   // differential_drive (utils/controllers.py:15-43, gains (3, 1000) landing.py:361) on a
   // kinematic unicycle; wheel speeds saturate at plat_speed / wheel radius (15 rad/s)
-  wpp = traj_point(a, ttype, tidx, sd);
   dx = wpp.x - S.plat.x; dy = wpp.y - S.plat.y;
+  float th = S.heading;
   float dth = map_to_pi(atan2f(dy, dx) - map_to_pi(th));
   if (fabsf(dth) < kDriveAngThresh) dth = 0.0f;
   float lin = sqrtf(dx * dx + dy * dy) * kDriveGainLin, ang = dth * kDriveGainAng;
@@ -447,8 +473,7 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
   sincosf(th, &sn, &cs);
   S.plat_v = make_float2(lin * cs, lin * sn);
   S.plat.x += S.plat_v.x * c.dt; S.plat.y += S.plat_v.y * c.dt;
-  sti(S.T, OUZ_I_TRAJ_IDX, tidx);
-  st(S.T, OUZ_F_PLAT_HEADING, th);
+  S.heading = th;
 }
 
 // ---------------------------------------------------------------------------
@@ -496,6 +521,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
   }
 
   OUZ_STAMP(2, false);
+  platform_prefetch<CTRL, TGT>(a, S);
   V3 f_b = v3(0.0f, 0.0f, 0.0f), tau_b = v3(0.0f, 0.0f, 0.0f);
   M3 R0;   // quat_to_mat of the (post-reset) state quaternion: shared by the controller and the integrator
 
@@ -506,8 +532,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
                   __fadd_rn(unit_f32(r.z), 1.0f));
     }
-    float4 act = reinterpret_cast<const float4*>(sc.actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
-    float av[4] = {act.x, act.y, act.z, act.w};
+    float av[4] = {S.act.x, S.act.y, S.act.z, S.act.w};
     if (a.drn_mask & 2) dr_noise_apply<4>(av, a.drn[1], a.seed, gid, sc.step, RNG_DRN_ACT);   // vec_task.py:323-325
     float eff[4];
     const bool on = tp.fault && S.progress >= S.fonset;
@@ -791,7 +816,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT>(a, i, tp, S);
+  if (valid) env_load<CTRL, TGT>(a, i, tp, S, ctx[0].actions);
   OUZ_STAMP(1, true);
   if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
@@ -817,6 +842,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
       const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
       if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
+      if (valid && k + 1 < K) load_actions<CTRL, TGT>(ctx[k + 1].actions, S);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i);
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
@@ -1018,6 +1044,57 @@ __global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, 
     out[1] = t[1];
     out[2] = t[2];
     *ticket = 0u;   // ready for the next launch on this stream
+  }
+}
+
+// The same statistics for n <= kStatsOneBlockEnvs: ONE block of 1024 threads strides over every env
+// (at 4096 envs four independent loads per field and thread, all in flight together) and reduces
+// through its waves in fixed order.  No partials, no device-scope fence, no ticket: the multi-block
+// form's fence + atomic + last-block pass made a 6 us kernel out of 48 KB of reads, 40 % of a
+// 16-step rollout's step time at 4096 envs.  Deterministic (fixed order), but not bitwise equal
+// to the multi-block form's order.
+constexpr int kStatsOneBlock = 1024;
+constexpr int kStatsOneBlockEnvs = 65536;
+
+__global__ void __launch_bounds__(kStatsOneBlock) episode_stats_one_block_kernel(StepArgs a, double* out, int drain) {
+  __shared__ double s_part[3][kStatsOneBlock / 64];
+  double acc[3] = {0.0, 0.0, 0.0};   // sum of returns, count, sum of lengths
+  constexpr int kUnroll = 4;
+  for (int base = threadIdx.x; base < a.n; base += kStatsOneBlock * kUnroll) {
+    float s[kUnroll];
+    int32_t c[kUnroll], l[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = base + u * kStatsOneBlock;
+      const bool ok = i < a.n;
+      s[u] = ok ? ld(a, OUZ_F_EP_SUM, i) : 0.0f;
+      c[u] = ok ? ldi(a, OUZ_I_EP_CNT, i) : 0;
+      l[u] = ok ? ldi(a, OUZ_I_EP_LEN, i) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int i = base + u * kStatsOneBlock;
+      acc[0] += (double)s[u];
+      acc[1] += (double)c[u];
+      acc[2] += (double)l[u];
+      if (drain && i < a.n) {
+        st(a, OUZ_F_EP_SUM, i, 0.0f);
+        sti(a, OUZ_I_EP_CNT, i, 0);
+        sti(a, OUZ_I_EP_LEN, i, 0);
+      }
+    }
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const double v = wave_sum(acc[k]);
+    if ((threadIdx.x & 63) == 0) s_part[k][w] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    double t = 0.0;
+    for (int j = 0; j < kStatsOneBlock / 64; ++j) t += s_part[threadIdx.x][j];
+    out[threadIdx.x] = t;
   }
 }
 
@@ -1487,6 +1564,12 @@ int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream) {
   if (!out) return fail(OUZ_ERR_INVALID, "ouz_episode_stats: null out");
   if (!env->cfg.track_episodes) return fail(OUZ_ERR_INVALID, "ouz_episode_stats: env created without track_episodes");
   const int n = env->cfg.num_envs;
+  if (n <= kStatsOneBlockEnvs) {
+    hipLaunchKernelGGL(episode_stats_one_block_kernel, dim3(1), dim3(kStatsOneBlock), 0, (hipStream_t)stream,
+                       env->args, out, drain ? 1 : 0);
+    OUZ_LAUNCH_CHECK("episode_stats_one_block_kernel");
+    return OUZ_OK;
+  }
   int grid = grid_for(n, kStatsBlock);
   if (grid > kStatsMaxBlocks) grid = kStatsMaxBlocks;
   hipLaunchKernelGGL(episode_stats_kernel, dim3(grid), dim3(kStatsBlock), 0, (hipStream_t)stream, env->args,
