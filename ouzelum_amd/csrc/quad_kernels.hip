@@ -755,6 +755,26 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
                                      float rew, bool rs, bool to, bool direct, bool keep_flags = false) {
   const uint32_t lane = (uint32_t)i & 63u;
   const uint32_t first = wave_tile(i) * 64u;   // wave-uniform: output bases live in SGPRs
+  if (n <= kLatencyRegimeEnvs && !direct) {
+    // Latency regime (a few waves per CU, the step is one dependent chain): each lane stores its own
+    // 52-byte row as three 16-byte stores + one dword (rows are 4-byte aligned; gfx950 global stores
+    // take dword alignment), skipping the LDS round trip and the wave barrier of the staged form.
+    // The staged form's full-line writes only pay off when HBM bandwidth is the bound.
+    if (valid) {
+      typedef float f4a4 __attribute__((ext_vector_type(4), aligned(4)));
+      float* row = o.obs + (size_t)i * OUZ_NUM_OBS;
+      *reinterpret_cast<f4a4*>(row) = f4a4{ob[0], ob[1], ob[2], ob[3]};
+      *reinterpret_cast<f4a4*>(row + 4) = f4a4{ob[4], ob[5], ob[6], ob[7]};
+      *reinterpret_cast<f4a4*>(row + 8) = f4a4{ob[8], ob[9], ob[10], ob[11]};
+      row[12] = ob[12];
+      (o.rew + first)[lane] = rew;
+      if (!(keep_flags && !rs)) {
+        (o.reset + first)[lane] = rs ? 1 : 0;
+        (o.timeouts + first)[lane] = to ? 1 : 0;
+      }
+    }
+    return;
+  }
   if (direct) {   // wave shared by two tasks (misaligned mixed shard): plain per-lane stores
     if (valid) {
 #pragma unroll
