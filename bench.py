@@ -175,11 +175,11 @@ def main():
         done = 0
         while done < steps:
             k = min(RING, steps - done)
+            slot = red.slot(n_roll[0])
             if fused:   # learner-style rollout: 16 steps into (16, N, ...) storage, state kept in registers
-                env.rollout(ring, k, fused=True, storage=tuple(t[:k] for t in storage))
-            else:       # one kernel launch per VecTask.step
-                env.rollout(ring, k)
-            env.episode_stats(out=red.slot(n_roll[0]))
+                env.rollout(ring, k, fused=True, storage=tuple(t[:k] for t in storage), stats_out=slot)
+            else:       # one kernel launch per VecTask.step, then the episode statistics (one C call)
+                env.rollout(ring, k, stats_out=slot)
             red.submit(n_roll[0])
             n_roll[0] += 1
             done += k

@@ -19,7 +19,8 @@
  *                   = pre_physics_step + gym.simulate x controlFrequencyInv + post_physics_step
  *                                              tasks/ekf_lee_landed.py:308-530,620-685
  *   ouz_step_n      K consecutive VecTask.step calls over a ring of action batches, one launch each
- *                   (the train_vec.py:14-18 env-only loop)
+ *                   (the train_vec.py:14-18 env-only loop); ouz_step_n_stats adds the rollout's
+ *                   episode statistics (RecordEpisodeStatisticsTorch, PPO/utils.py:20-35)
  *   ouz_rollout     the same K steps fused into launches of up to 32 steps each: env state stays in
  *                   registers, per-step obs/rew/reset/time_outs go to rollout storage [K][N][...]
  *                   (the learners' obs[step] = next_obs buffers, PPO/main.py:67-73,88-96) or to the
@@ -212,6 +213,11 @@ int ouz_reset_all(ouz_env* env, void* stream);
  * per-step host bookkeeping (PPO/utils.py:20-35); the pair is what config E
  * all-reduces over RCCL (sum and count; the lengths give info["l"]). */
 int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream);
+/* ouz_step_n followed by ouz_episode_stats in one call: the rollout shape of the learners
+ * (T env steps, then RecordEpisodeStatisticsTorch's returns, PPO/utils.py:20-35 /
+ * RPO-LSTM/main.py:96-110) for one host call per rollout instead of two. */
+int ouz_step_n_stats(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, double* stats_out,
+                     int32_t drain, void* stream);
 
 /* Per-step trace of one env + per-step reset counts, written by the step kernel
  * itself (no extra launch, no host sync).  Feeds the reference's trajectory CSV

@@ -96,6 +96,7 @@ SIGNATURES = {
     "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
     "ouz_reset_all": (_I, [_P, _P]),
     "ouz_episode_stats": (_I, [_P, _P, _I, _P]),
+    "ouz_step_n_stats": (_I, [_P, _P, _I, _I, _P, _I, _P]),
     "ouz_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
     "ouz_get_step": (_I64, [_P]),

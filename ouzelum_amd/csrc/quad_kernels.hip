@@ -1598,6 +1598,16 @@ int ouz_episode_stats(ouz_env* env, double* out, int32_t drain, void* stream) {
   return OUZ_OK;
 }
 
+int ouz_step_n_stats(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, double* stats_out,
+                     int32_t drain, void* stream) {
+  if (!stats_out) return fail(OUZ_ERR_INVALID, "ouz_step_n_stats: null stats_out");
+  if (env && !env->cfg.track_episodes)
+    return fail(OUZ_ERR_INVALID, "ouz_step_n_stats: env created without track_episodes");
+  const int rc = ouz_step_n(env, ring, ring_len, n_steps, stream);
+  if (rc) return rc;
+  return ouz_episode_stats(env, stats_out, drain, stream);
+}
+
 int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity) {
   if (!env) return fail(OUZ_ERR_INVALID, "ouz_set_trace: null env");
   if (capacity == 0) {

@@ -312,7 +312,7 @@ class QuadVecTask:
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
 
-    def rollout(self, action_ring, n_steps, fused=False, storage=None):
+    def rollout(self, action_ring, n_steps, fused=False, storage=None, stats_out=None, drain=True):
         """``n_steps`` consecutive VecTask.step calls over a ring of pre-staged action batches
         ``(T, N, 4)`` (``None`` for the Lee tasks, which ignore actions) with one C call.
 
@@ -320,7 +320,16 @@ class QuadVecTask:
         steps per launch with the env state held in registers (``ouz_rollout``); with
         ``storage=(obs (K,N,13), rew (K,N), reset (K,N) int64, time_outs (K,N) bool)`` every
         step's outputs land in the learner's rollout buffers, the env buffers keep the last step.
+        ``stats_out`` (a float64 device tensor of >= 3): also write the episode statistics after
+        the last step, as ``episode_stats(drain, out=stats_out)`` would (``ouz_step_n_stats``: one
+        host call for the steps and the statistics).
         """
+        if stats_out is not None:
+            if not self.cfg.track_episodes:
+                raise RuntimeError("create the env with track_episodes=True")
+            if (stats_out.dtype != torch.float64 or stats_out.numel() < 3 or not stats_out.is_contiguous()
+                    or stats_out.device != self.device):
+                raise ValueError("stats_out must be a contiguous float64 tensor of >= 3 on the env device")
         if action_ring is None:
             ring_ptr, ring_len = None, 1
             if self.uses_actions:
@@ -333,7 +342,11 @@ class QuadVecTask:
         if not fused:
             if storage is not None:
                 raise ValueError("storage needs fused=True")
-            L.check(L.lib.ouz_step_n(self._env, ring_ptr, ring_len, int(n_steps), self._stream()), "ouz_step_n")
+            if stats_out is not None:
+                L.check(L.lib.ouz_step_n_stats(self._env, ring_ptr, ring_len, int(n_steps), L.ptr(stats_out),
+                                               1 if drain else 0, self._stream()), "ouz_step_n_stats")
+            else:
+                L.check(L.lib.ouz_step_n(self._env, ring_ptr, ring_len, int(n_steps), self._stream()), "ouz_step_n")
             return
         ptrs = [None] * 4
         if storage is not None:
@@ -348,6 +361,8 @@ class QuadVecTask:
                     raise ValueError(f"storage {name} must be {shape} {dt}")
             ptrs = [L.ptr(obs), L.ptr(rew), L.ptr(rst), L.ptr(to)]
         L.check(L.lib.ouz_rollout(self._env, ring_ptr, ring_len, int(n_steps), *ptrs, self._stream()), "ouz_rollout")
+        if stats_out is not None:
+            self.episode_stats(drain, out=stats_out)
 
     def reset(self):
         """vec_task.py:377-389: returns the current obs, does not touch the simulation."""

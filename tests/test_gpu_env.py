@@ -311,6 +311,38 @@ def test_episode_stats_kernel(ouz, task, n):
     assert float(env.episode_stats()[1]) == 0.0          # drained
 
 
+def test_episode_stats_into_return_ring(ouz):
+    """bench.py's per-rollout pattern: the rollout's statistics into ReturnAllReduce's double-buffered ring
+    (rollout(stats_out=slot) or episode_stats(out=slot); single process: no collective) give the same
+    [sum, count, lengths] as the by-reference buffer of a separate env."""
+    from ouzelum_amd.distributed import ReturnAllReduce
+    n = 2048
+    a = ouz.make(seed=9, task="QuadFault", num_envs=n, sim_device="cuda:0", track_episodes=True)
+    b = ouz.make(seed=9, task="QuadFault", num_envs=n, sim_device="cuda:0", track_episodes=True)
+    ring = (torch.rand((16, n, 4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 2 - 1)
+    red = ReturnAllReduce(torch.device("cuda:0"))
+    assert not red.active
+    got, want = [], []
+    for r in range(6):
+        if r % 2:   # steps + statistics in one C call (ouz_step_n_stats), as bench.py does
+            a.rollout(ring, 16, stats_out=red.slot(r))
+        else:
+            a.rollout(ring, 16)
+            out = a.episode_stats(out=red.slot(r))
+            assert out.data_ptr() == red.slots[r % 2].data_ptr()
+        b.rollout(ring, 16)
+        red.submit(r)
+        got.append(red.result(r).clone())
+        want.append(b.episode_stats().clone())
+    red.finish()
+    assert torch.equal(torch.stack(got), torch.stack(want))
+    assert float(torch.stack(want)[:, 1].sum()) > 0
+    with pytest.raises(ValueError):
+        a.episode_stats(out=torch.zeros(3, device="cuda"))          # float32: rejected
+    with pytest.raises(ValueError):
+        a.rollout(ring, 4, stats_out=torch.zeros(2, dtype=torch.float64, device="cuda"))   # too short
+
+
 def test_rlgames_creator_and_max_episode_override(ouz):
     """A task YAML with maxEpisodeLength 30 (cfg/task/*.yaml) through the rl_games creator: the
     time-outs fire where the oracle's do, at progress 29 (vec_task.py:348-351)."""
