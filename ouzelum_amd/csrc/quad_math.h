@@ -457,7 +457,10 @@ OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
     x[3] = o[0]; x[4] = o[1]; x[5] = o[2];
   }
   const T q_a = (T)kPvAccVar;
-  const M3T<T> MMt = mmt(M, M);
+  // G Q Gᵀ = q_a [[h² M Mᵀ, h dt M Mᵀ], [dt h M Mᵀ, dt² M Mᵀ]] with M a rotation: M Mᵀ = I up to the
+  // f32 rounding of M (~1e-7, the same as in the reference's own f32 product), so the noise term is
+  // diagonal and the 27-FMA f64 product is not formed.
+  const M3T<T> MMt{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
   M3T<T> T13 = madd(pblk(P, 0, 2), mm(M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2)))));
   M3T<T> T12 = madd(pblk(P, 0, 1), mm(M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1)))));
   {
@@ -477,7 +480,10 @@ OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
 //   S = P_mm + r I;  K_o = P_om S^-1 (o != m)
 //   x_m = z - r S^-1 y;  x_o += K_o y
 //   P_mm = r (I - r S^-1);  P_mo = r S^-1 P_mo = r K_o^T;  P_oo' = P_oo' - K_o P_mo'
-template <int MB, typename T>
+// R0 = true: the velocity fix as the reference runs it, R = 0 (PVFilter.py:76-79 tests gps_var): the
+// r-scaled terms are exact zeros (x_m = z, P_mm = P_mo = 0), written as zeros instead of computed as
+// 0 * (products) — IEEE f64 cannot fold 0 * x, so the generic form pays ~40 f64 operations for them.
+template <int MB, typename T, bool R0 = false>
 OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
   constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
   constexpr int B = 2;
@@ -490,13 +496,13 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
   const M3T<T> KA = mm(pblk(P, A, MB), Si), KB = mm(pblk(P, B, MB), Si);     // K_o = P_{o,m} S^-1
   {
     T y[3] = {z[0] - x[MB * 3 + 0], z[1] - x[MB * 3 + 1], z[2] - x[MB * 3 + 2]};
-    T sy[3], dA[3], dB[3];
-    mva(Si, y, sy);
+    T sy[3] = {T(0), T(0), T(0)}, dA[3], dB[3];
+    if constexpr (!R0) mva(Si, y, sy);
     mva(KA, y, dA);
     mva(KB, y, dB);
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      x[MB * 3 + k] = z[k] - r * sy[k];
+      x[MB * 3 + k] = R0 ? z[k] : z[k] - r * sy[k];
       x[A * 3 + k] += dA[k];
       x[B * 3 + k] += dB[k];
     }
@@ -505,10 +511,17 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
   pset(P, B, B, msub(pblk(P, B, B), mm(KB, pblk(P, MB, B))));
   pset(P, A, B, msub(pblk(P, A, B), mm(KA, pblk(P, MB, B))));
   pset(P, A, A, msub(pblk(P, A, A), mm(KA, pblk(P, MB, A))));
-  if (MB < A) pset(P, MB, A, mscale(r, tr(KA))); else pset(P, A, MB, mscale(r, KA));
-  pset(P, MB, B, mscale(r, tr(KB)));
-  M3T<T> I3{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
-  pset(P, MB, MB, mscale(r, msub(I3, mscale(r, Si))));
+  if constexpr (R0) {
+    const M3T<T> Z{{T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0)}};
+    if (MB < A) pset(P, MB, A, Z); else pset(P, A, MB, Z);
+    pset(P, MB, B, Z);
+    pset(P, MB, MB, Z);
+  } else {
+    if (MB < A) pset(P, MB, A, mscale(r, tr(KA))); else pset(P, A, MB, mscale(r, KA));
+    pset(P, MB, B, mscale(r, tr(KB)));
+    M3T<T> I3{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
+    pset(P, MB, MB, mscale(r, msub(I3, mscale(r, Si))));
+  }
 }
 
 // One PV-filter step as the driver runs it (ekf_lee_landed.py:417-444): predict, then the
@@ -533,7 +546,7 @@ OUZ_HD void pv_step(float xf[9], float Pf[45], V3 acc, EkfQ q, float dt, bool po
   }
   if (vel_fix) {
     const PvReal z[3] = {(PvReal)zv.x, (PvReal)zv.y, (PvReal)zv.z};
-    pv_correct_t<1, PvReal>(x, P, z, PvReal(0));
+    pv_correct_t<1, PvReal, true>(x, P, z, PvReal(0));
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k) xf[k] = (float)x[k];
