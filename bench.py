@@ -156,7 +156,9 @@ def main():
     rank, world, local = init_from_env()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    dev = torch.device("cuda", local)
+    # one GPU per rank (torchrun's LOCAL_RANK); modulo the device count so an N-rank rehearsal with
+    # OUZ_DIST_BACKEND=gloo can share one GPU
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     n = args.num_envs
     off, total = shard(n, rank, world)

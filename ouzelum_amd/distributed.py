@@ -21,7 +21,9 @@ def init_from_env(backend=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # OUZ_DIST_BACKEND=gloo: rehearse the N > 1 path with several ranks on one GPU (RCCL wants
+            # one GPU per rank); the product path is "nccl" = RCCL over xGMI
+            backend = os.environ.get("OUZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
