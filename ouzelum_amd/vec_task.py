@@ -114,6 +114,8 @@ class QuadVecTask:
         self.states_buf = torch.zeros((n, 0), dtype=torch.float32, device=self.device)
         self.extras = {}
         self.obs_dict = {}
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._act_shape = torch.Size((n, L.NUM_ACT))
 
         handle = ctypes.c_void_p()
         L.check(L.lib.ouz_create(cfg, handle), "ouz_create")
@@ -296,6 +298,13 @@ class QuadVecTask:
     def _actions_ptr(self, actions):
         if actions is None:
             return L.ptr(self._zero_actions)
+        # fast path (the learners' case: a contiguous f32 (N, 4) tensor on this device) in a few C calls;
+        # everything else goes through the checks and conversion below
+        if (type(actions) is torch.Tensor and actions.dtype is torch.float32 and actions.is_cuda
+                and actions.get_device() == self._dev_index and actions.shape == self._act_shape
+                and actions.is_contiguous()):
+            self._last_actions = actions   # keep alive until the kernel has read it
+            return actions.data_ptr()
         if not isinstance(actions, torch.Tensor):
             raise TypeError("actions must be a torch tensor")
         if actions.shape != (self.num_envs, self.num_actions):
@@ -307,7 +316,9 @@ class QuadVecTask:
 
     def step(self, actions):
         """VecTask.step (vec_task.py:313-359): clamp -> pre -> simulate -> post -> timeouts -> obs clamp."""
-        L.check(L.lib.ouz_step(self._env, self._actions_ptr(actions), self._stream()), "ouz_step")
+        rc = L.lib.ouz_step(self._env, self._actions_ptr(actions), L.stream_ptr(self._dev_index))
+        if rc:
+            L.check(rc, "ouz_step")
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
