@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "philox.h"
 
 namespace ouz {
@@ -91,13 +93,28 @@ OUZ_HD M3T<T> mscale(T s, const M3T<T>& A) { M3T<T> C;
 #pragma unroll
   for (int k = 0; k < 9; ++k) C.m[k] = s * A.m[k]; return C; }
 
+// 1 / x.  On the device, f64: the hardware reciprocal estimate refined by two Newton steps (full
+// double precision for the normal, positive determinants of SPD 3x3 blocks) instead of the
+// correctly rounded division sequence (div_scale / div_fmas / div_fixup), ~2x fewer f64 issues.
+template <typename T>
+OUZ_HD T recip(T x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same_v<T, double>) {
+    double y = __builtin_amdgcn_rcp(x);
+    y = y * (2.0 - x * y);
+    return y * (2.0 - x * y);
+  }
+#endif
+  return T(1) / x;
+}
+
 // Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).
 template <typename T>
 OUZ_HD M3T<T> inv_sym3(const M3T<T>& S) {
   T a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
   T A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
   T D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
-  T inv_det = T(1) / (a * A + b * B + c * C);
+  T inv_det = recip<T>(a * A + b * B + c * C);
   return M3T<T>{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
                  C * inv_det, E * inv_det, F * inv_det}};
 }
