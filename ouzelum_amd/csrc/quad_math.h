@@ -108,6 +108,45 @@ OUZ_HD T recip(T x) {
   return T(1) / x;
 }
 
+// Accumulating products, each entry ONE fma chain seeded with the accumulator: C + A B, C + A B^T and
+// C - A B.  (madd(C, mm(A, B)) is a mul, two fmas and an add per entry: the compiler may not
+// reassociate the add into the chain.)
+template <typename T>
+OUZ_HD M3T<T> mm_add(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
+  M3T<T> R;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      R.m[i * 3 + j] = fma(A.m[i * 3 + 2], B.m[2 * 3 + j], fma(A.m[i * 3 + 1], B.m[1 * 3 + j],
+                           fma(A.m[i * 3 + 0], B.m[0 * 3 + j], C.m[i * 3 + j])));
+  return R;
+}
+template <typename T>
+OUZ_HD M3T<T> mmt_add(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
+  M3T<T> R;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      R.m[i * 3 + j] = fma(A.m[i * 3 + 2], B.m[j * 3 + 2], fma(A.m[i * 3 + 1], B.m[j * 3 + 1],
+                           fma(A.m[i * 3 + 0], B.m[j * 3 + 0], C.m[i * 3 + j])));
+  return R;
+}
+template <typename T>
+OUZ_HD M3T<T> mm_sub(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
+  M3T<T> R;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      R.m[i * 3 + j] = fma(-A.m[i * 3 + 2], B.m[2 * 3 + j], fma(-A.m[i * 3 + 1], B.m[1 * 3 + j],
+                           fma(-A.m[i * 3 + 0], B.m[0 * 3 + j], C.m[i * 3 + j])));
+  return R;
+}
+template <typename T>
+OUZ_HD M3T<T> diag3(T d) { return M3T<T>{{d, T(0), T(0), T(0), d, T(0), T(0), T(0), d}}; }
+
 // Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).
 template <typename T>
 OUZ_HD M3T<T> inv_sym3(const M3T<T>& S) {
@@ -476,18 +515,17 @@ OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
   const T q_a = (T)kPvAccVar;
   // G Q Gᵀ = q_a [[h² M Mᵀ, h dt M Mᵀ], [dt h M Mᵀ, dt² M Mᵀ]] with M a rotation: M Mᵀ = I up to the
   // f32 rounding of M (~1e-7, the same as in the reference's own f32 product), so the noise term is
-  // diagonal and the 27-FMA f64 product is not formed.
-  const M3T<T> MMt{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
-  M3T<T> T13 = madd(pblk(P, 0, 2), mm(M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2)))));
-  M3T<T> T12 = madd(pblk(P, 0, 1), mm(M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1)))));
+  // diagonal (diag3 below) and the 27-FMA f64 product is not formed.
+  M3T<T> T13 = mm_add(pblk(P, 0, 2), M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2))));
+  M3T<T> T12 = mm_add(pblk(P, 0, 1), M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1))));
   {
-    M3T<T> T11 = madd(pblk(P, 0, 0), mm(M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0)))));
-    pset(P, 0, 0, madd(madd(T11, mmt(madd(mscale(dt, T12), mscale(h, T13)), M)), mscale(q_a * h * h, MMt)));
+    M3T<T> T11 = mm_add(pblk(P, 0, 0), M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0))));
+    pset(P, 0, 0, mmt_add(madd(T11, diag3(q_a * h * h)), madd(mscale(dt, T12), mscale(h, T13)), M));
   }
-  pset(P, 0, 1, madd(mmt(madd(T12, mscale(dt, T13)), M), mscale(q_a * h * dt, MMt)));
+  pset(P, 0, 1, mmt_add(diag3(q_a * h * dt), madd(T12, mscale(dt, T13)), M));
   M3T<T> T23 = mm(M, madd(pblk(P, 1, 2), mscale(dt, pblk(P, 2, 2))));
   M3T<T> T22 = mm(M, madd(pblk(P, 1, 1), mscale(dt, pblk(P, 2, 1))));
-  pset(P, 1, 1, madd(mmt(madd(T22, mscale(dt, T23)), M), mscale(q_a * dt * dt, MMt)));
+  pset(P, 1, 1, mmt_add(diag3(q_a * dt * dt), madd(T22, mscale(dt, T23)), M));
   pset(P, 0, 2, T13);
   pset(P, 1, 2, T23);
 }
@@ -525,9 +563,9 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
     }
   }
   // other-other blocks first: they read P_{m,o}, which is overwritten below
-  pset(P, B, B, msub(pblk(P, B, B), mm(KB, pblk(P, MB, B))));
-  pset(P, A, B, msub(pblk(P, A, B), mm(KA, pblk(P, MB, B))));
-  pset(P, A, A, msub(pblk(P, A, A), mm(KA, pblk(P, MB, A))));
+  pset(P, B, B, mm_sub(pblk(P, B, B), KB, pblk(P, MB, B)));
+  pset(P, A, B, mm_sub(pblk(P, A, B), KA, pblk(P, MB, B)));
+  pset(P, A, A, mm_sub(pblk(P, A, A), KA, pblk(P, MB, A)));
   if constexpr (R0) {
     const M3T<T> Z{{T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0)}};
     if (MB < A) pset(P, MB, A, Z); else pset(P, A, MB, Z);
