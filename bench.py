@@ -187,13 +187,21 @@ def main():
             done += k
         red.finish()
 
+    ev = {}
+
     def timed(steps, fused=False):
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
+        # HIP events on the stream the step kernels run on (torch's current stream: the env launches
+        # on it), bracketing the timed region: GPU time per step including the per-rollout statistics
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
+        e0.record()
         rollouts(steps, fused)
+        e1.record()
         torch.cuda.synchronize(dev)
+        ev["fused" if fused else "steps"] = e0.elapsed_time(e1) * 1e3 / steps
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
@@ -229,7 +237,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    us = kernel_time_us(env, ring)
+    us_b2b = kernel_time_us(env, ring)
+    us = ev["steps"]
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
@@ -238,7 +247,11 @@ def main():
                                "dt 0.01 x 2 sub-steps",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
                    "parallelism": f"env-sharded dp{world} (async RCCL return all-reduce per 16-step rollout)"},
-        "roofline": roofline_entry(args.task, n, us),
+        "roofline": {**roofline_entry(args.task, n, us),
+                     "kernel_us_source": "HIP events on the step stream around the timed region / steps "
+                                         "(includes the per-rollout episode statistics)",
+                     "kernel_us_back_to_back": round(us_b2b, 3),
+                     "regime": "latency-bound: 4096 envs' state is L2/MALL-resident, see roofline_sweep"},
         "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
     }
     if value_fused is not None:
