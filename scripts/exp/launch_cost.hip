@@ -34,12 +34,39 @@ template <int N> double gpu_us(hipStream_t s, int* out, int reps) {
   return ms * 1e3 / reps;
 }
 
+// same launches through hipModuleLaunchKernel on a hipFunction_t resolved once (no per-launch
+// host-function lookup), arguments as one buffer (extra) or as a parameter array
+template <int N> double host_us_module(hipStream_t s, int* out, int reps, bool buffer) {
+  struct { Blob<N> a; int* o; } args{};
+  args.o = out;
+  size_t size = sizeof(args);
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &args, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  void* params[] = {&args.a, &args.o};
+  hipFunction_t f;
+  (void)hipGetFuncBySymbol(&f, reinterpret_cast<const void*>(&empty_kernel<N>));
+  spin_kernel<<<1, 64, 0, s>>>(200000000LL);
+  auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0; k < reps; ++k)
+    (void)hipModuleLaunchKernel(f, 64, 1, 1, 64, 1, 1, 0, s, buffer ? nullptr : params, buffer ? extra : nullptr);
+  auto t1 = std::chrono::steady_clock::now();
+  (void)hipStreamSynchronize(s);
+  return std::chrono::duration<double, std::micro>(t1 - t0).count() / reps;
+}
+
 int main() {
   hipStream_t s; (void)hipStreamCreate(&s);
   int* out; (void)hipMalloc(&out, 4096 * sizeof(int)); (void)hipMemset(out, 0, 4096 * sizeof(int));
   for (int w = 0; w < 3; ++w) host_us<16>(s, out, 200);
   printf("host us/launch: 16B %.3f  256B %.3f  640B %.3f  1152B %.3f  2048B %.3f\n", host_us<16>(s, out, 400),
          host_us<256>(s, out, 400), host_us<640>(s, out, 400), host_us<1152>(s, out, 400), host_us<2048>(s, out, 400));
+  for (int w = 0; w < 3; ++w) host_us_module<16>(s, out, 200, true);
+  printf("host us/module-launch (extra buffer): 16B %.3f  256B %.3f  640B %.3f  1152B %.3f\n",
+         host_us_module<16>(s, out, 400, true), host_us_module<256>(s, out, 400, true),
+         host_us_module<640>(s, out, 400, true), host_us_module<1152>(s, out, 400, true));
+  printf("host us/module-launch (param array):  16B %.3f  256B %.3f  640B %.3f  1152B %.3f\n",
+         host_us_module<16>(s, out, 400, false), host_us_module<256>(s, out, 400, false),
+         host_us_module<640>(s, out, 400, false), host_us_module<1152>(s, out, 400, false));
+  printf("host us/launch again: 16B %.3f  640B %.3f\n", host_us<16>(s, out, 400), host_us<640>(s, out, 400));
   printf("gpu  us/launch: 16B %.3f  256B %.3f  640B %.3f  1152B %.3f  2048B %.3f\n", gpu_us<16>(s, out, 400),
          gpu_us<256>(s, out, 400), gpu_us<640>(s, out, 400), gpu_us<1152>(s, out, 400), gpu_us<2048>(s, out, 400));
   // graph of 16 dependent launches: host cost per replay and GPU time per node
