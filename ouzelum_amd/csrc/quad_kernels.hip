@@ -36,7 +36,7 @@ constexpr int kLatencyRegimeEnvs = 65536;
 // Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
 // single-step kernel, read back with ouz_probe_stamps.  Not part of the product library.
 #ifdef OUZ_PROBE_STAMPS
-constexpr int kStampSlots = 12, kStampWaves = 1024;
+constexpr int kStampSlots = 13, kStampWaves = 1024;
 __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
 #define OUZ_STAMP(k, wait)                                                                       \
   do {                                                                                           \
@@ -598,7 +598,9 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       float inv = 1.0f / sqrtf(S.eq.w * S.eq.w + S.eq.x * S.eq.x + S.eq.y * S.eq.y + S.eq.z * S.eq.z);
       S.eq = EkfQ{S.eq.w * inv, S.eq.x * inv, S.eq.y * inv, S.eq.z * inv};
     }
+    OUZ_STAMP(10, false);
     ekf_update(S.eq, S.eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
+    OUZ_STAMP(11, false);
     EkfQ orient = S.eq;
     float pm[3] = {S.p.x, S.p.y, S.p.z}, vm[3] = {S.v.x, S.v.y, S.v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
     if (conv) {
@@ -627,6 +629,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       pv_step(S.px, S.pP, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
               g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
       __asm__ volatile("" ::: "memory");
+      OUZ_STAMP(12, false);
 #pragma unroll
       for (int k = 0; k < kPark; ++k) vals[k] = pk[k * kMaxBlock];
       S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);

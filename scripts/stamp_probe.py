@@ -1,7 +1,8 @@
 """Phase timeline of the single-step kernel from per-wave s_memtime stamps (probe build:
 OUZ_EXTRA_FLAGS=-DOUZ_PROBE_STAMPS).  Stamps: 0 entry, 1 state loads landed, 2 reset done,
 3 controller done, 4 integrator done, 5 env_core done, 6 obs emitted, 7 stores landed;
-8 / 9 s_memrealtime (100 MHz) at entry / exit."""
+8 / 9 s_memrealtime (100 MHz) at entry / exit; estimator tasks: 10 / 11 around the AHRS-EKF update,
+12 after the PV-filter step."""
 import ctypes
 import sys
 
@@ -21,15 +22,16 @@ acts = (torch.rand((n, 4), device="cuda") * 2 - 1).contiguous()
 for _ in range(300):
     env.step(acts)
 torch.cuda.synchronize()
+SLOTS = 13
 waves = min((n + 63) // 64, 1024)
 rows = []
 for rep in range(40):
     for _ in range(25):
         env.step(acts)
     torch.cuda.synchronize()
-    buf = np.zeros(1024 * 12, dtype=np.uint64)
+    buf = np.zeros(1024 * SLOTS, dtype=np.uint64)
     assert lib.ouz_probe_stamps(buf.ctypes.data, buf.size) > 0
-    rows.append(buf.reshape(1024, 12)[:waves].astype(np.int64))
+    rows.append(buf.reshape(1024, SLOTS)[:waves].astype(np.int64))
 st = np.concatenate(rows, 0)
 names = ["loads", "reset", "controller", "physics", "post/obs/reward", "emit", "store+drain"]
 d = np.diff(st[:, :8], axis=1)
@@ -45,3 +47,8 @@ skew = [int(x.max() - x.min()) * 10 for x in per_launch]
 span = [int(r[:, 9].max() - r[:, 8].min()) * 10 for r in rows]
 print(f"  wave start skew within a launch: median {np.median(skew):.0f} ns; first start -> last exit {np.median(span):.0f} ns")
 print(f"  implied clock (cycles / realtime): {np.median(tot / np.maximum(rt, 1)) / 10:.2f} GHz")
+if st[:, 12].any():
+    sub = [("ctrl: inputs -> EKF", st[:, 10] - st[:, 2]), ("ctrl: AHRS-EKF update", st[:, 11] - st[:, 10]),
+           ("ctrl: PV filter step", st[:, 12] - st[:, 11]), ("ctrl: guidance + Lee", st[:, 3] - st[:, 12])]
+    for nm, v in sub:
+        print(f"  {nm:24s} {np.median(v):8.0f} {np.percentile(v, 90):8.0f}")
