@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--sweep", default="4194304,16777216")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-fused", action="store_true", help="skip the fused-rollout measurement")
+    ap.add_argument("--allreduce-batch", type=int, default=8,
+                    help="16-step rollouts whose return statistics share one all-reduce (N > 1)")
     return ap.parse_args()
 
 
@@ -176,9 +178,10 @@ def main():
     storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
                torch.empty((RING, n), dtype=torch.int64, device=dev), torch.empty((RING, n), dtype=torch.bool, device=dev))
 
-    # per-rollout return all-reduce (RCCL when N > 1), asynchronous on the collective's stream and
-    # double-buffered so the next rollout's steps do not wait for it (distributed.ReturnAllReduce)
-    red = ReturnAllReduce(dev)
+    # per-rollout return statistics all-reduced (RCCL when N > 1) asynchronously on the collective's
+    # stream, double-buffered so the next rollouts' steps do not wait for it, and ARB rollouts' rows per
+    # collective: one dist.all_reduce call costs ~20 us of host time (distributed.ReturnAllReduce)
+    red = ReturnAllReduce(dev, batch=args.allreduce_batch)
     n_roll = [0]
 
     def rollouts(steps, fused=False):
@@ -254,7 +257,8 @@ def main():
         "config": {"workload": f"config B: {n}-env x500 hover, Lee position controller ({args.task}), fp32, "
                                "dt 0.01 x 2 sub-steps",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
-                   "parallelism": f"env-sharded dp{world} (async RCCL return all-reduce per 16-step rollout)"},
+                   "parallelism": f"env-sharded dp{world} (per-16-step-rollout return statistics, async RCCL "
+                                  f"all-reduce of {args.allreduce_batch} rollouts' rows per collective)"},
         "roofline": {**roofline_entry(args.task, n, us),
                      "kernel_us_source": "HIP events on the step stream around the timed region / steps "
                                          "(includes the per-rollout episode statistics)",

@@ -51,41 +51,62 @@ class ReturnAllReduce:
     ``allreduce_returns`` is blocking in stream order: the next rollout's step kernels wait for
     the collective (an 8-byte RCCL all-reduce over xGMI is latency-bound, ~10-30 us on 8 GPUs,
     i.e. several 4096-env steps).  Nothing the env does depends on the reduced value, so this
-    helper keeps ``depth`` stat slots: rollout r's stats go to slot r % depth and are all-reduced
-    asynchronously on the collective's own stream while the next rollouts step; a slot is only
-    reused after its previous all-reduce has completed (``wait`` orders the current stream after
-    it, which by then has long finished).  ``result(r)`` returns the global [sum, count, ...]
-    of rollout r once it is done.
+    helper keeps ``depth`` blocks of ``batch`` stat rows: rollout r's stats go to row r % batch of
+    block (r // batch) % depth, and a block is all-reduced asynchronously, in ONE collective, once
+    its last row is submitted, on the collective's own stream while the next rollouts step.  One
+    call of ``dist.all_reduce`` costs ~20 us of host time (RCCL, measured in
+    ``profiles/r01/allreduce_host.txt``), as much as five 4096-env steps, so ``batch`` rollouts
+    share it; the per-rollout global statistics are unchanged.  A block is only reused after its
+    collectives have completed (``wait`` orders the current stream after them).  ``result(r)``
+    returns the global [sum, count, ...] of rollout r, flushing the rows not yet reduced first;
+    every rank must make the same calls in the same order (they are collectives).
     """
 
-    def __init__(self, device, depth=2, width=3):
-        self.slots = torch.zeros((depth, width), dtype=torch.float64, device=device)
-        self.works = [None] * depth
-        self.depth = depth
+    def __init__(self, device, depth=2, width=3, batch=1):
+        if depth < 1 or batch < 1:
+            raise ValueError("depth and batch must be >= 1")
+        self.slots = torch.zeros((depth, batch, width), dtype=torch.float64, device=device)
+        self.depth, self.batch = depth, batch
+        self.works = [[] for _ in range(depth)]
+        self.lo = [0] * depth       # first row of the block not yet in a submitted collective
+        self.filled = [0] * depth   # rows of the block submitted by the caller
         self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 
+    def _where(self, r):
+        return (r // self.batch) % self.depth, r % self.batch
+
+    def _wait(self, d):
+        for w in self.works[d]:
+            w.wait()
+        self.works[d] = []
+
+    def _flush(self, d, hi):
+        if self.active and self.lo[d] < hi:
+            self.works[d].append(dist.all_reduce(self.slots[d, self.lo[d]:hi], op=dist.ReduceOp.SUM,
+                                                 async_op=True))
+        self.lo[d] = max(self.lo[d], hi)
+
     def slot(self, r):
-        """The output slot for rollout r (waits for that slot's previous all-reduce first)."""
-        k = r % self.depth
-        if self.works[k] is not None:
-            self.works[k].wait()
-            self.works[k] = None
-        return self.slots[k]
+        """The output row for rollout r (a block's first row waits for that block's previous collectives)."""
+        d, row = self._where(r)
+        if row == 0:
+            self._wait(d)
+            self.lo[d] = self.filled[d] = 0
+        return self.slots[d, row]
 
     def submit(self, r):
-        k = r % self.depth
-        if self.active:
-            self.works[k] = dist.all_reduce(self.slots[k], op=dist.ReduceOp.SUM, async_op=True)
+        d, row = self._where(r)
+        self.filled[d] = max(self.filled[d], row + 1)
+        if row == self.batch - 1:
+            self._flush(d, self.batch)
 
     def finish(self):
-        for k, w in enumerate(self.works):
-            if w is not None:
-                w.wait()
-                self.works[k] = None
+        for d in range(self.depth):
+            self._flush(d, self.filled[d])
+            self._wait(d)
 
     def result(self, r):
-        k = r % self.depth
-        if self.works[k] is not None:
-            self.works[k].wait()
-            self.works[k] = None
-        return self.slots[k]
+        d, row = self._where(r)
+        self._flush(d, row + 1)
+        self._wait(d)
+        return self.slots[d, row]

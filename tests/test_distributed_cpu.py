@@ -136,26 +136,44 @@ def _async_worker(rank, world, port, out_dir):
                       LOCAL_RANK=str(rank))
     from ouzelum_amd.distributed import ReturnAllReduce, init_from_env
     init_from_env(backend="gloo")
-    red = ReturnAllReduce(torch.device("cpu"), depth=2)
-    assert red.active
-    got = []
-    for r in range(7):   # bench.py's pattern: fill slot r % 2, submit, keep stepping; read back later
+
+    def fill(red, r):
         red.slot(r).copy_(torch.tensor([10.0 * r + rank, 1.0 + rank, float(r)], dtype=torch.float64))
         red.submit(r)
-        if r >= 1:
-            got.append(red.result(r - 1).clone())
-    got.append(red.result(6).clone())
-    red.finish()
-    torch.save(torch.stack(got), os.path.join(out_dir, f"a{rank}.pt"))
+
+    for batch in (1, 3):
+        # bench.py's pattern: fill the rollout's row, submit, keep stepping; read the previous one back
+        red = ReturnAllReduce(torch.device("cpu"), depth=2, batch=batch)
+        assert red.active
+        got = []
+        for r in range(7):
+            fill(red, r)
+            if r >= 1:
+                got.append(red.result(r - 1).clone())
+        got.append(red.result(6).clone())
+        red.finish()
+        torch.save(torch.stack(got), os.path.join(out_dir, f"a{rank}_b{batch}.pt"))
+        # rows read only after finish(): 11 rollouts in blocks of 4 -> two full blocks' collectives and
+        # a partial one flushed by finish(); depth 3 keeps all of them
+        red = ReturnAllReduce(torch.device("cpu"), depth=3, batch=batch + 1)
+        for r in range(11):
+            fill(red, r)
+        red.finish()
+        torch.save(torch.stack([red.result(r).clone() for r in range(11) if r // (batch + 1) >= 11 // (batch + 1) - 2]),
+                   os.path.join(out_dir, f"f{rank}_b{batch}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_async_return_allreduce(tmp_path):
-    """ReturnAllReduce (the double-buffered asynchronous per-rollout all-reduce of bench.py) gives every
-    rank the global [sum, count, ...] of each rollout, and a slot is not overwritten while in flight."""
+    """ReturnAllReduce (the asynchronous per-rollout all-reduce of bench.py, ``batch`` rollouts' rows per
+    collective) gives every rank the global [sum, count, ...] of each rollout, flushes rows read before
+    their block is full exactly once, and a row is not overwritten while in flight."""
     mp.spawn(_async_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    a0 = torch.load(tmp_path / "a0.pt", weights_only=True)
-    a1 = torch.load(tmp_path / "a1.pt", weights_only=True)
-    want = torch.tensor([[20.0 * r + 1, 3.0, 2.0 * r] for r in range(7)], dtype=torch.float64)
-    assert torch.equal(a0, want) and torch.equal(a1, want)
+    want = torch.tensor([[20.0 * r + 1, 3.0, 2.0 * r] for r in range(11)], dtype=torch.float64)
+    for batch in (1, 3):
+        for rank in (0, 1):
+            assert torch.equal(torch.load(tmp_path / f"a{rank}_b{batch}.pt", weights_only=True), want[:7])
+            b = batch + 1
+            keep = [r for r in range(11) if r // b >= 11 // b - 2]
+            assert torch.equal(torch.load(tmp_path / f"f{rank}_b{batch}.pt", weights_only=True), want[keep])
