@@ -117,6 +117,16 @@ class PPOLearner:
     def initial_state(self):
         return self.actor.initial_state(self.num_envs, self.device) if self.recurrent else None
 
+    def act(self, state, lstm_state=None, done=None):
+        """``get_action`` for one rollout step, replayed from a hipGraph on the GPU (``GraphedPolicy``)
+        unless ``OUZ_GRAPH_POLICY=0``.  The outputs are the graph's static tensors, overwritten by
+        the next call: copy what must outlive it (the rollout loop stores them into its buffers)."""
+        if self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "0") != "1":
+            return self.get_action(state, lstm_state, done)
+        if getattr(self, "_graphed", None) is None:
+            self._graphed = GraphedPolicy(self)
+        return self._graphed(state, lstm_state, done)
+
     @torch.no_grad()
     def get_gae(self, next_obs, next_done, rewards, dones, values):
         next_value = self.critic(next_obs).reshape(-1)
@@ -211,3 +221,49 @@ class PPOLearner:
         self.actor.load_state_dict(torch.load(filename + "_actor", map_location=m, weights_only=True))
         self.actor_optimizer.load_state_dict(torch.load(filename + "_actor_optimizer", map_location=m,
                                                         weights_only=True))
+
+
+class GraphedPolicy:
+    """The rollout step's policy call (trunk MLP, input projection, LSTM GEMM + fused cell kernel,
+    mean head, Normal sample, log-prob, entropy: ~25 launches) captured once in a hipGraph and
+    replayed per step.  Eagerly each of those launches costs several µs of host time, ~440 µs per
+    4096-env step in all, 100x the env step; a replay is one host call.
+
+    Inputs are copied into static buffers before each replay; the parameters are read in place
+    (Adam updates them in place, so every replay sees the current policy); the Normal sample draws
+    from torch's graph-safe Philox stream.  The LSTM carry returned is the graph's output buffer and
+    is copied into the input buffer by the next call.
+    """
+
+    def __init__(self, learner, warmup=3):
+        self.learner = learner
+        self.warmup = warmup
+        self.graph = None
+
+    def _capture(self, state, lstm_state, done):
+        ln = self.learner
+        self.s_in = state.detach().clone()
+        self.s_done = done.detach().clone()
+        self.s_lstm = (lstm_state[0].detach().clone(), lstm_state[1].detach().clone()) if ln.recurrent else None
+        side = torch.cuda.Stream(device=ln.device)
+        side.wait_stream(torch.cuda.current_stream(ln.device))
+        with torch.cuda.stream(side):   # warm-up: lazy workspaces / kernels resolved outside the capture
+            for _ in range(self.warmup):
+                ln.get_action(self.s_in, self.s_lstm, self.s_done)
+        torch.cuda.current_stream(ln.device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        # relaxed: the caching allocator may map a fresh segment for the graph's private pool during
+        # the capture (hipMalloc), which the default "global" mode rejects on ROCm
+        with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
+            self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done)
+
+    def __call__(self, state, lstm_state, done):
+        if self.graph is None:
+            self._capture(state, lstm_state, done)
+        self.s_in.copy_(state)
+        self.s_done.copy_(done)
+        if self.s_lstm is not None:
+            self.s_lstm[0].copy_(lstm_state[0])
+            self.s_lstm[1].copy_(lstm_state[1])
+        self.graph.replay()
+        return self.out

@@ -96,7 +96,7 @@ def train(args):
             obs[step] = next_obs
             dones[step] = next_done
             act_in = pomdp if args.rollout_obs == "pomdp" else next_obs
-            action, logprob, _, lstm_state = agent.get_action(act_in, lstm_state, next_done)
+            action, logprob, _, lstm_state = agent.act(act_in, lstm_state, next_done)
             actions[step] = action
             logprobs[step] = logprob
             next_obs, rewards[step], next_done, info = envs.step(action)
@@ -152,7 +152,7 @@ def play(args):
     lstm = agent.initial_state()
     rewards = []
     for _ in range(max(1, args.total_steps // N)):
-        action, _, _, lstm = agent.get_action(next_obs, lstm, next_done)
+        action, _, _, lstm = agent.act(next_obs, lstm, next_done)
         next_obs, rew, next_done, _ = env.step(action)
         rewards.append(rew.mean())
         if not args.quiet:

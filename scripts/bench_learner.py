@@ -51,7 +51,7 @@ for it in range(a.warmup + a.iters):
         pomdps[s] = pomdp
         obs[s] = next_obs
         dones[s] = next_done
-        act, lp, _, lstm = agent.get_action(next_obs, lstm, next_done)
+        act, lp, _, lstm = agent.act(next_obs, lstm, next_done)
         actions[s] = act
         logprobs[s] = lp
         next_obs, rewards[s], next_done, info = env.step(act)

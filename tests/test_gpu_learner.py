@@ -136,3 +136,47 @@ def test_fused_lstm_and_splitk_gradients_match_torch():
     errs = {k: float((grads[0][k] - grads[1][k]).abs().max() / grads[1][k].abs().max().clamp_min(1e-6))
             for k in grads[1]}
     assert max(errs.values()) < 2e-4, errs
+
+
+@pytest.mark.parametrize("recurrent", [True, False])
+def test_graphed_policy_matches_eager(recurrent):
+    """PPOLearner.act (the rollout step's policy replayed from a hipGraph) against the eager policy
+    over 20 replays with changing inputs, done resets and an in-place parameter update in between:
+    the LSTM carry is bit-identical, the log-prob of the sampled action is the eager Normal's, and
+    the samples are fresh draws each replay."""
+    from ouzelum_amd.learners import PPOLearner
+    from ouzelum_amd.learners.models import run_mlp
+    from ouzelum_amd.spaces import Box
+    dev = torch.device("cuda:0")
+    N = 1024
+    obs_space = Box(-np.inf * np.ones(13), np.inf * np.ones(13))
+    act_space = Box(-np.ones(4), np.ones(4))
+    torch.manual_seed(5)
+    agent = PPOLearner(obs_space, act_space, N, dev, recurrent=recurrent)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    lstm = agent.initial_state()
+    ref_lstm = None if lstm is None else (lstm[0].clone(), lstm[1].clone())
+    prev = None
+    for k in range(20):
+        state = torch.randn((N, 13), device=dev, generator=g)
+        done = (torch.rand(N, device=dev, generator=g) < 0.2).float()
+        if k == 10:   # an optimizer step in between: the graph reads the parameters in place
+            with torch.no_grad():
+                for p in agent.actor.parameters():
+                    p.add_(0.01 * torch.randn(p.shape, device=dev, generator=g))
+        action, logprob, entropy, lstm = agent.act(state, lstm, done)
+        with torch.no_grad():
+            if recurrent:
+                hidden, want_lstm = agent.actor.get_states(state, ref_lstm, done)
+                mean = agent.actor.actor_mean(hidden)
+                assert torch.equal(lstm[0], want_lstm[0]) and torch.equal(lstm[1], want_lstm[1])
+                ref_lstm = (want_lstm[0].clone(), want_lstm[1].clone())
+            else:
+                mean = run_mlp(agent.actor.actor_mean, state)
+            std = torch.exp(agent.actor.actor_logstd.expand_as(mean))
+            want_lp = torch.distributions.Normal(mean, std, validate_args=False).log_prob(action).sum(1)
+        torch.testing.assert_close(logprob, want_lp, rtol=1e-5, atol=1e-5)
+        assert torch.isfinite(action).all() and torch.isfinite(entropy).all()
+        if prev is not None:
+            assert not torch.equal(action, prev)
+        prev = action.clone()
