@@ -50,9 +50,9 @@ class MLPActor(nn.Module):
         )
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
 
-    def forward(self, state, action=None):
+    def forward(self, state, action=None, eps=None):
         mean = run_mlp(self.actor_mean, state)
-        return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha)
+        return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps)
 
 
 class LSTMActor(nn.Module):
@@ -111,19 +111,22 @@ class LSTMActor(nn.Module):
             outs.append(h)
         return torch.cat(outs, 0), (h.unsqueeze(0), c.unsqueeze(0))
 
-    def forward(self, state, lstm_state, done, action=None):
+    def forward(self, state, lstm_state, done, action=None, eps=None):
         hidden, lstm_state = self.get_states(state, lstm_state, done)
         mean = self.actor_mean(hidden)    # 128 -> 4: too small for the split-K path
-        return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha), lstm_state)
+        return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps), lstm_state)
 
 
-def _policy_head(mean, logstd, action, rpo_alpha):
+def _policy_head(mean, logstd, action, rpo_alpha, eps=None):
     # validate_args=False: the default argument check is a device->host sync on every call (and
-    # cannot be captured in a hipGraph); mean / std are finite by construction
+    # cannot be captured in a hipGraph); mean / std are finite by construction.  The sample is
+    # mean + std * eps, eps ~ N(0, 1) (given by the caller, or drawn here): Normal.sample() calls
+    # torch.normal(mean_tensor, std_tensor), whose std >= 0 check is a std.min().item() device->host
+    # sync on every call, and which cannot be captured in a hipGraph
     std = torch.exp(logstd.expand_as(mean))
     if action is None:
         probs = Normal(mean, std, validate_args=False)
-        action = probs.sample()
+        action = mean + std * (torch.randn_like(mean) if eps is None else eps)
     else:
         if rpo_alpha > 0.0:   # RPO: perturb the mean for the policy update (RPO-LSTM/model.py:61-64)
             mean = mean + torch.empty_like(mean).uniform_(-rpo_alpha, rpo_alpha)

@@ -109,10 +109,10 @@ class PPOLearner:
 
     # ------------------------------------------------------------------ rollout
     @torch.no_grad()
-    def get_action(self, state, lstm_state=None, done=None):
+    def get_action(self, state, lstm_state=None, done=None, eps=None):
         if self.recurrent:
-            return self.actor(state, lstm_state, done)
-        return (*self.actor(state), None)
+            return self.actor(state, lstm_state, done, eps=eps)
+        return (*self.actor(state, eps=eps), None)
 
     def initial_state(self):
         return self.actor.initial_state(self.num_envs, self.device) if self.recurrent else None
@@ -121,7 +121,7 @@ class PPOLearner:
         """``get_action`` for one rollout step, replayed from a hipGraph on the GPU (``GraphedPolicy``)
         unless ``OUZ_GRAPH_POLICY=0``.  The outputs are the graph's static tensors, overwritten by
         the next call: copy what must outlive it (the rollout loop stores them into its buffers)."""
-        if self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "0") != "1":
+        if self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "1") == "0":
             return self.get_action(state, lstm_state, done)
         if getattr(self, "_graphed", None) is None:
             self._graphed = GraphedPolicy(self)
@@ -230,8 +230,9 @@ class GraphedPolicy:
     4096-env step in all, 100x the env step; a replay is one host call.
 
     Inputs are copied into static buffers before each replay; the parameters are read in place
-    (Adam updates them in place, so every replay sees the current policy); the Normal sample draws
-    from torch's graph-safe Philox stream.  The LSTM carry returned is the graph's output buffer and
+    (Adam updates them in place, so every replay sees the current policy).  The sample's standard
+    normal draws are made by ``normal_`` into a static buffer before each replay (models._policy_head:
+    the sample is mean + std * eps).  The LSTM carry returned is the graph's output buffer and
     is copied into the input buffer by the next call.
     """
 
@@ -245,23 +246,25 @@ class GraphedPolicy:
         self.s_in = state.detach().clone()
         self.s_done = done.detach().clone()
         self.s_lstm = (lstm_state[0].detach().clone(), lstm_state[1].detach().clone()) if ln.recurrent else None
+        self.s_eps = torch.zeros((state.shape[0], ln.actor.actor_logstd.shape[1]), device=ln.device)
         side = torch.cuda.Stream(device=ln.device)
         side.wait_stream(torch.cuda.current_stream(ln.device))
         with torch.cuda.stream(side):   # warm-up: lazy workspaces / kernels resolved outside the capture
             for _ in range(self.warmup):
-                ln.get_action(self.s_in, self.s_lstm, self.s_done)
+                ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
         torch.cuda.current_stream(ln.device).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
         # relaxed: the caching allocator may map a fresh segment for the graph's private pool during
-        # the capture (hipMalloc), which the default "global" mode rejects on ROCm
+        # the capture
         with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
-            self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done)
+            self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
 
     def __call__(self, state, lstm_state, done):
         if self.graph is None:
             self._capture(state, lstm_state, done)
         self.s_in.copy_(state)
         self.s_done.copy_(done)
+        self.s_eps.normal_()
         if self.s_lstm is not None:
             self.s_lstm[0].copy_(lstm_state[0])
             self.s_lstm[1].copy_(lstm_state[1])

@@ -139,7 +139,7 @@ def test_fused_lstm_and_splitk_gradients_match_torch():
 
 
 @pytest.mark.parametrize("recurrent", [True, False])
-def test_graphed_policy_matches_eager(recurrent):
+def test_graphed_policy_matches_eager(recurrent, monkeypatch):
     """PPOLearner.act (the rollout step's policy replayed from a hipGraph) against the eager policy
     over 20 replays with changing inputs, done resets and an in-place parameter update in between:
     the LSTM carry is bit-identical, the log-prob of the sampled action is the eager Normal's, and
@@ -147,6 +147,7 @@ def test_graphed_policy_matches_eager(recurrent):
     from ouzelum_amd.learners import PPOLearner
     from ouzelum_amd.learners.models import run_mlp
     from ouzelum_amd.spaces import Box
+    monkeypatch.setenv("OUZ_GRAPH_POLICY", "1")
     dev = torch.device("cuda:0")
     N = 1024
     obs_space = Box(-np.inf * np.ones(13), np.inf * np.ones(13))
@@ -180,3 +181,4 @@ def test_graphed_policy_matches_eager(recurrent):
         if prev is not None:
             assert not torch.equal(action, prev)
         prev = action.clone()
+    assert agent._graphed is not None and agent._graphed.graph is not None
