@@ -1,22 +1,32 @@
-"""Env-steps/s of the fused HIP quadrotor step (BASELINE.json metric), one process per GPU.
+"""Env-steps/s of the HIP quadrotor step (BASELINE.json metric), one process per GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--task LeeLanded] [--num-envs 4096]
     torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N ...
 
-A "step" is one VecTask.step of the hot path over one batch of ``num_envs`` envs
-per GPU (config B of BASELINE.json by default: 4096-env x500 hover with the Lee
-controller, fp32).  Actions come from a ring of 16 synthetic batches staged in
-HBM before timing (train_vec.py:14-18 draws random actions; the Lee tasks
-ignore them, ekf_lee_landed.py:308).  Episodic returns are accumulated in-kernel
-and, once per 16-step rollout, reduced on device and all-reduced over RCCL when
-N > 1 — the single collective of the path.  Weak scaling: every
-rank simulates ``num_envs`` envs of the global id range.
+A "step" is one VecTask.step of the hot path (vec_task.py:313-359) over one batch
+of ``num_envs`` envs per GPU: config B of BASELINE.json by default (4096-env x500
+hover with the Lee position controller, fp32).  Actions come from a ring of 16
+synthetic batches staged in HBM before timing (train_vec.py:14-18 draws random
+actions; the Lee tasks ignore them, ekf_lee_landed.py:308).
 
-Rank 0 prints ONE JSON line.  ``roofline`` prices the step kernel at the bench
-workload; ``roofline_sweep`` repeats it at large N where the state no longer
-fits the 256 MiB Infinity Cache (at 4096 envs the whole state is
-cache-resident, so an HBM fraction there means nothing).  ``cpu_baseline`` times
-the float64 numpy oracle (oracle/quad_oracle.py, "port") on a bounded sample.
+The timed loop runs the env the way a rollout collector does (RPO-LSTM/main.py:89-110:
+T env steps, then RecordEpisodeStatisticsTorch's returns): each 16-step rollout is
+ONE persistent launch (``ouz_rollout_stats``) that steps every env 16 times with its
+state in registers, writes every step's obs / rew / reset / time_outs into (16, N, ...)
+rollout storage, and reduces the rollout's finished-episode statistics in the same
+launch; when N > 1 those statistics are all-reduced over RCCL (asynchronously, a
+block of rollouts per collective) -- the single collective of the path.
+The same steps as one ``quad_step_kernel`` launch per step (the ``VecTask.step``
+call, ``ouz_step``) are measured beside it (``per_step_launch``).  Weak scaling:
+every rank simulates ``num_envs`` envs of the global id range.
+
+Rank 0 prints ONE JSON line.  ``roofline`` prices the headline kernel at the bench
+workload from HIP events on its stream; ``roofline_sweep`` repeats the pricing at
+large N, where the state no longer fits the 256 MiB Infinity Cache (at
+4096 envs the whole state is cache-resident, so an HBM fraction there means little).
+``configs`` carries the other single-GPU BASELINE configs (C, D and E's per-GPU
+shard) measured the same way.  ``cpu_baseline`` times the float64 numpy oracle
+(oracle/quad_oracle.py, "port") on all host cores, before the GPU is touched.
 """
 import argparse
 import json
@@ -33,20 +43,29 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (4096 envs) + achieved HBM GB/s vs roofline, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-RING = 16
+RING = 16                       # rollout length (RPO-LSTM rollout_steps = 16) and action-ring depth
 
-# Algorithmic bytes per env-step of quad_step_kernel<TASK>: every
-# field the kernel must read and write per env, SoA f32 / i32, obs AoS f32,
-# reset i64, timeouts u8.  Reset-only and done-only traffic is excluded.
-# reset r, p/q/v/w r+w, progress r+w, obs w, rew w, timeouts r (reset / timeouts are written only
-# when an env is or was done: a few % of env-steps, excluded like the other done-only traffic)
+# BASELINE.json configs measured on one GPU: (letter, task, envs per GPU, description)
+CONFIGS = {
+    "B": ("LeeLanded", 4096, "x500 hover, Lee position controller on true state, fp32"),
+    "C": ("QuadTracking", 4096, "trajectory tracking + AHRS-EKF + PV-KF + domain randomisation, fp32 (PV step f64)"),
+    "D": ("QuadFault", 8192, "RL per-rotor thrust + single-rotor fault + obs noise, recurrent-PPO obs, fp32"),
+    "E": ("QuadMixed", 4096, "per-GPU shard of the 32768-env mixed hover/tracking/fault curriculum, fp32"),
+}
+TASK_CONFIG = {task: letter for letter, (task, _, _) in CONFIGS.items()}
+
+# Algorithmic bytes per env-step of quad_step_kernel<TASK>: every field the kernel must
+# read and write per env, SoA f32 / i32, obs AoS f32, reset i64, timeouts u8.  Reset-only and done-only
+# traffic is excluded.  reset r, p/q/v/w r+w, progress r+w, obs w, rew w, timeouts r (reset / timeouts are
+# written only when an env is or was done: a few % of env-steps, excluded like the other done-only traffic)
 _CORE = 8 + 52 + 4 + 52 + 4 + 52 + 4 + 1
+_RL_ACT = 16
 BYTES_PER_ENV_STEP = {
     "LeeLanded": _CORE,
     # + random-goal target (12 r/w), rotor thrusts (16 r/w), actions (16 r)
-    "Ouzelum": _CORE + 2 * 12 + 2 * 16 + 16,
+    "Ouzelum": _CORE + 2 * 12 + 2 * 16 + _RL_ACT,
     # + fault rotor / onset / eta (12 r)
-    "QuadFault": _CORE + 2 * 12 + 2 * 16 + 16 + 12,
+    "QuadFault": _CORE + 2 * 12 + 2 * 16 + _RL_ACT + 12,
     # + prev_v (12), EKF q + packed P (56), PV x + packed P (216), waypoint (12), each r/w
     "EKFLeeLanded": _CORE + 2 * (12 + 56 + 216 + 12),
     # + DR scales (12 r), platform xy + heading (12 r/w), trajectory type / index / scale (12 r, 4 w)
@@ -55,6 +74,18 @@ BYTES_PER_ENV_STEP = {
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0
 EPISODE_TRACK_BYTES = 8           # ep_ret r/w when track_episodes is on
+_STEP_OUT = 52 + 4 + 8 + 1        # one step's obs / rew / reset i64 / time_outs u8 (rollout storage row)
+_USES_ACTIONS = {"Ouzelum": 1.0, "QuadFault": 1.0, "QuadMixed": 1.0 / 3.0}
+
+
+def rollout_bytes_per_env_step(task, k=RING):
+    """Algorithmic bytes per env-step of one K-step quad_rollout_kernel launch with rollout storage and fused
+    statistics: every step writes its storage row (65 B) and reads its action row (RL tasks); the env state
+    (everything the per-step kernel reads and writes besides its outputs and actions) is read and written once
+    per launch, plus the env buffers' last-step row (65 B) and the episode accumulators (12 B r)."""
+    act = _RL_ACT * _USES_ACTIONS.get(task, 0.0)
+    state = BYTES_PER_ENV_STEP[task] - 52 - 4 - act + EPISODE_TRACK_BYTES
+    return _STEP_OUT + act + (state + _STEP_OUT + 12) / k
 
 
 def parse():
@@ -67,51 +98,68 @@ def parse():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other single-GPU BASELINE configs")
     ap.add_argument("--sweep", default="4194304,16777216")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--no-fused", action="store_true", help="skip the fused-rollout measurement")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="total budget of the CPU baseline leg")
     ap.add_argument("--allreduce-batch", type=int, default=8,
                     help="16-step rollouts whose return statistics share one all-reduce (N > 1)")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------------------------------- CPU baseline
+def cpu_baseline_leg(task, n, seed, budget_s):
+    """The float64 numpy oracle on every host core of this box (oracle/cpu_bench.py), at the bench workload
+    and at N = 64 / 4096 / 8192 for configs B and C, plus the reference-structure per-env estimator loop.
+    Runs before the GPU is initialised (the worker processes are forked)."""
+    from oracle import cpu_bench as C
+    cores = C.host_cores()
+    sizes = [64, 4096, 8192]
+    runs = [("B", "LeeLanded", s) for s in sizes] + [("C", "QuadTracking", s) for s in sizes]
+    if (task, n) not in {(t, s) for _, t, s in runs}:
+        runs.insert(0, (TASK_CONFIG.get(task, "-"), task, n))
+    per = budget_s * 0.85 / len(runs)
+    table = []
+    for letter, t, s in runs:
+        r = C.vectorised(t, s, seed=seed, budget_s=per, cores=cores)
+        r["config"] = letter
+        table.append(r)
+        print(f"cpu baseline: {t} {s} envs on {r['cores']} cores: {r['value']:.4g} env-steps/s", file=sys.stderr,
+              flush=True)
+    head = next(r for r in table if r["task"] == task and r["num_envs"] == n)
+    ref = C.reference_structure(n=16, budget_s=budget_s * 0.15)
+    return {"value": head["value"], "unit": "env-steps/s", "cores": head["cores"], "kind": "port",
+            "sample": head["sample"] + f"; host {C.host_model()}, {cores} cores available (sched_getaffinity)",
+            "host_cores": cores, "host_model": C.host_model(), "table": table,
+            "reference_structure_estimator": {**ref, "config": "C"}}
+
+
+# ----------------------------------------------------------------------------------------- GPU side
 def make_env(task, n, dev, seed, off, total):
     from ouzelum_amd import QuadVecTask
     return QuadVecTask(task=task, num_envs=n, sim_device=str(dev), rl_device=str(dev), seed=seed,
                        env_id_offset=off, num_envs_total=total, track_episodes=True)
 
 
-def action_ring(n, dev, seed):
+def action_ring(n, dev, seed, depth=RING):
     g = torch.Generator(device=dev).manual_seed(seed)
-    return (torch.rand((RING, n, 4), device=dev, generator=g) * 2 - 1).contiguous()
+    return (torch.rand((depth, n, 4), device=dev, generator=g) * 2 - 1).contiguous()
 
 
-def kernel_time_us(env, ring, reps=200, fused=False):
-    """Average duration of one step kernel from HIP events on the stream the kernel runs on.
-
-    The stream is first held by a spin kernel so that all ``reps`` launches (one
-    ``ouz_step_n`` C loop) are queued before the GPU reaches them; the bracket then
-    holds ``reps`` back-to-back kernels and no host launch gap, i.e. kernel time plus
-    the ~1 us dependent-launch boundary (MI355X_MICROARCH.md 'boundary' row)."""
-    dev = env.device
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(dev)
+def spin():
+    """Hold the stream so the launches that follow queue up before the GPU reaches them."""
     try:
         torch.cuda._sleep(int(2e7))
     except Exception:  # noqa: BLE001
         pass
-    s.record()
-    env.rollout(ring, reps, fused=fused)
-    e.record()
-    torch.cuda.synchronize(dev)
-    return s.elapsed_time(e) * 1e3 / reps
 
 
-def load_traffic(task, n):
-    """HBM bytes per launch of this kernel at this size from the committed PMC summary
-    (scripts/gpu_pmc.sh: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes), or None."""
+def load_traffic(kernel, task, n):
+    """HBM bytes per launch of this kernel at this size from the committed PMC summary (scripts/gpu_pmc.sh:
+    FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes), or None."""
     import glob
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_*_{task}_{n}_summary.json")))
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_*_{kernel}_{task}_{n}_summary.json")))
+    if not hits and kernel == "step":   # round-1 summaries of the per-step kernel carry no kernel tag
+        hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r01", f"pmc_r01_{task}_{n}_summary.json")))
     if not hits:
         return None
     with open(hits[-1]) as fh:
@@ -119,100 +167,80 @@ def load_traffic(task, n):
     t = d.get("traffic_bytes_per_launch")
     if not t:
         return None
+    steps = d.get("steps_per_launch", 1)
     raw = d.get("fetch_size_kb_raw")
-    return {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / n, 2),
-            # split of the total: reads are FETCH_SIZE x2 (the guide's gfx950 correction for wide
-            # streaming reads), writes WRITE_SIZE; the uncorrected read figure is kept beside it
-            "read_bytes_per_env_step": round(d["read_bytes_corrected"] / n, 2),
-            "read_bytes_per_env_step_uncorrected": round(raw * 1024 / n, 2) if raw else None,
-            "write_bytes_per_env_step": round(d["write_bytes"] / n, 2),
+    return {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / (n * steps), 2),
+            "read_bytes_per_env_step": round(d["read_bytes_corrected"] / (n * steps), 2),
+            "read_bytes_per_env_step_uncorrected": round(raw * 1024 / (n * steps), 2) if raw else None,
+            "write_bytes_per_env_step": round(d["write_bytes"] / (n * steps), 2),
             "source": os.path.relpath(hits[-1], ROOT)}
 
 
-def roofline_entry(task, n, us, track=True):
-    b = BYTES_PER_ENV_STEP[task] + (EPISODE_TRACK_BYTES if track else 0)
-    achieved = b * n / (us * 1e-6) / 1e9
-    traffic = load_traffic(task, n)
+def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
+    """``us_per_step``: GPU time per env-step batch; a launch covers ``steps_per_launch`` steps."""
+    b = (rollout_bytes_per_env_step(task, steps_per_launch) if kernel == "rollout"
+         else BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES)
+    achieved = b * n / (us_per_step * 1e-6) / 1e9
+    traffic = load_traffic(kernel, task, n)
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
-            "num_envs": n, "bytes_per_env_step": b, "kernel_us": round(us, 3)}
+            "kernel": "quad_rollout_kernel" if kernel == "rollout" else "quad_step_kernel",
+            "steps_per_launch": steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
+            "bytes_per_launch": round(b * n * steps_per_launch), "kernel_us": round(us_per_step, 3),
+            "kernel_us_per_launch": round(us_per_step * steps_per_launch, 3)}
 
 
-def cpu_baseline(task, n, seed, budget_s):
-    from oracle import quad_oracle as Q
-    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=seed))
-    rs = np.random.RandomState(0)
-    acts = rs.uniform(-1, 1, (RING, n, 4))
-    for k in range(3):                       # warm-up (first steps allocate)
-        o.step(acts[k % RING])
-    t0 = time.perf_counter()
-    for k in range(5):
-        o.step(acts[k % RING])
-    per = (time.perf_counter() - t0) / 5
-    steps = int(max(5, min(20000, budget_s / max(per, 1e-6))))
-    t0 = time.perf_counter()
-    for k in range(steps):
-        o.step(acts[k % RING])
-    el = time.perf_counter() - t0
-    return {"value": round(n * steps / el, 1), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/quad_oracle.py OracleEnv float64 numpy, task={task}, {n} envs x {steps} steps "
-                      f"({el:.1f} s, 1 thread)"}
+class Runner:
+    """One env driven by 16-step rollouts: fused (``ouz_rollout_stats``, the headline) or one launch per step
+    (``ouz_step_n_stats``, the VecTask.step path).  Statistics go to ``red``'s slots."""
 
+    def __init__(self, task, n, dev, seed, rank, world, red):
+        off, total = rank * n, world * n
+        self.env = make_env(task, n, dev, seed, off, total)
+        self.ring = action_ring(n, dev, seed + rank)
+        self.storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
+                        torch.empty((RING, n), dtype=torch.int64, device=dev),
+                        torch.empty((RING, n), dtype=torch.bool, device=dev))
+        self.red = red
+        self.plans = {}
+        self.n_roll = 0
+        self.dev = dev
+        self.n = n
 
-def main():
-    args = parse()
-    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env, shard
-    rank, world, local = init_from_env()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # one GPU per rank (torchrun's LOCAL_RANK); modulo the device count so an N-rank rehearsal with
-    # OUZ_DIST_BACKEND=gloo can share one GPU
-    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
-    torch.cuda.set_device(dev)
-    n = args.num_envs
-    off, total = shard(n, rank, world)
-    env = make_env(args.task, n, dev, args.seed, off, total)
-    ring = action_ring(n, dev, args.seed + rank)
+    def plan(self, k):
+        if k not in self.plans:
+            self.plans[k] = self.env.rollout_plan(self.ring, k, storage=tuple(t[:k] for t in self.storage))
+        return self.plans[k]
 
-    storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
-               torch.empty((RING, n), dtype=torch.int64, device=dev), torch.empty((RING, n), dtype=torch.bool, device=dev))
-
-    # per-rollout return statistics all-reduced (RCCL when N > 1) asynchronously on the collective's
-    # stream, double-buffered so the next rollouts' steps do not wait for it, and ARB rollouts' rows per
-    # collective: one dist.all_reduce call costs ~20 us of host time (distributed.ReturnAllReduce)
-    red = ReturnAllReduce(dev, batch=args.allreduce_batch)
-    n_roll = [0]
-
-    def rollouts(steps, fused=False):
+    def rollouts(self, steps, fused=True):
         done = 0
+        red = self.red
         while done < steps:
             k = min(RING, steps - done)
-            slot = red.slot(n_roll[0])
-            if fused:   # learner-style rollout: 16 steps into (16, N, ...) storage, state kept in registers
-                env.rollout(ring, k, fused=True, storage=tuple(t[:k] for t in storage), stats_out=slot)
-            else:       # one kernel launch per VecTask.step, then the episode statistics (one C call)
-                env.rollout(ring, k, stats_out=slot)
-            red.submit(n_roll[0])
-            n_roll[0] += 1
+            r = self.n_roll
+            if fused:
+                self.plan(k)(red.slot_ptr(r))
+            else:
+                self.env.rollout(self.ring, k, stats_out=red.slot(r))
+            red.submit(r)
+            self.n_roll += 1
             done += k
         red.finish()
 
-    ev = {}
-
-    def timed(steps, fused=False):
+    def timed(self, steps, world, fused=True):
+        """Wall seconds (max over ranks) and GPU us per step from HIP events on the step stream."""
+        dev = self.dev
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
-        # HIP events on the stream the step kernels run on (torch's current stream: the env launches
-        # on it), bracketing the timed region: GPU time per step including the per-rollout statistics
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record()
-        rollouts(steps, fused)
+        self.rollouts(steps, fused)
         e1.record()
         torch.cuda.synchronize(dev)
-        ev["fused" if fused else "steps"] = e0.elapsed_time(e1) * 1e3 / steps
+        gpu_us = e0.elapsed_time(e1) * 1e3 / steps
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
@@ -220,27 +248,124 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        return el
+        return el, gpu_us
 
-    rollouts(args.warmup)
-    el = timed(args.steps)
-    value = n * world * args.steps / el
-    value_fused = el_fused = None
-    if not args.no_fused:
-        rollouts(args.warmup, fused=True)
-        el_fused = timed(args.steps, fused=True)
-        value_fused = n * world * args.steps / el_fused
+    def back_to_back_us(self, fused=True, launches=40):
+        """GPU time per step of back-to-back launches queued behind a spin kernel (no host gap): kernel time
+        plus the ~1 us dependent-launch boundary (MI355X_MICROARCH.md 'boundary' row)."""
+        dev = self.dev
+        torch.cuda.synchronize(dev)
+        buf = torch.zeros(3, dtype=torch.float64, device=dev)
+        p = self.plan(RING)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        spin()
+        s.record()
+        if fused:
+            for _ in range(launches):
+                p(buf.data_ptr())
+            steps = launches * RING
+        else:
+            steps = launches * 5
+            self.env.rollout(self.ring, steps)
+        e.record()
+        torch.cuda.synchronize(dev)
+        return s.elapsed_time(e) * 1e3 / steps
 
-    # secondary: the same steps through the Python VecTask.step() API (one ctypes call each)
-    py_rate = None
-    if rank == 0:
+
+def measure(task, n, dev, seed, rank, world, args, red, with_per_step=True):
+    """Headline-style measurement of one config: fused rollouts (timed), then the per-step launch path."""
+    run = Runner(task, n, dev, seed, rank, world, red)
+    run.rollouts(max(args.warmup, 1))
+    el, gpu_us = run.timed(args.steps, world)
+    out = {"value": n * world * args.steps / el, "ms_per_step": el / args.steps * 1e3, "kernel_us": gpu_us}
+    if with_per_step:
+        run.rollouts(max(args.warmup, 1), fused=False)
+        el2, gpu2 = run.timed(args.steps, world, fused=False)
+        out["per_step"] = {"value": n * world * args.steps / el2, "ms_per_step": el2 / args.steps * 1e3,
+                           "kernel_us": gpu2}
+    return run, out
+
+
+def sweep_entries(task, sizes, dev, seed):
+    """Both kernels priced at large N (state >> 256 MiB MALL), back-to-back launches behind a spin kernel."""
+    out = []
+    for big in sizes:
+        e2 = make_env(task, big, dev, seed, 0, big)
+        r2 = action_ring(big, dev, seed, depth=2)
+        e2.rollout(r2, 20)
         torch.cuda.synchronize(dev)
-        k = min(args.steps, 500)
-        t0 = time.perf_counter()
-        for i in range(k):
-            env.step(ring[i % RING])
+        reps = 30 if big <= (1 << 22) else 12
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        spin()
+        s.record()
+        e2.rollout(r2, reps)
+        e.record()
         torch.cuda.synchronize(dev)
-        py_rate = n * k / (time.perf_counter() - t0)
+        out.append(roofline_entry("step", task, big, s.elapsed_time(e) * 1e3 / reps))
+        # the fused rollout at the same size: 16 steps per launch into (16, N, ...) storage + fused statistics
+        st = (torch.empty((RING, big, 13), device=dev), torch.empty((RING, big), device=dev),
+              torch.empty((RING, big), dtype=torch.int64, device=dev),
+              torch.empty((RING, big), dtype=torch.bool, device=dev))
+        ring16 = action_ring(big, dev, seed)
+        p = e2.rollout_plan(ring16, RING, storage=st)
+        buf = torch.zeros(3, dtype=torch.float64, device=dev)
+        p(buf.data_ptr())
+        torch.cuda.synchronize(dev)
+        launches = 3
+        spin()
+        s.record()
+        for _ in range(launches):
+            p(buf.data_ptr())
+        e.record()
+        torch.cuda.synchronize(dev)
+        out.append(roofline_entry("rollout", task, big, s.elapsed_time(e) * 1e3 / (launches * RING), RING))
+        del e2, r2, st, ring16
+        torch.cuda.empty_cache()
+    return out
+
+
+def config_entry(letter, task, n, res, run, sweep=None):
+    us_b2b = run.back_to_back_us(fused=True)
+    us_b2b_step = run.back_to_back_us(fused=False)
+    e = {"config": letter, "task": task, "num_envs_per_gpu": n, "value": round(res["value"], 1),
+         "unit": "env-steps/s", "ms_per_step": round(res["ms_per_step"], 5),
+         "roofline": {**roofline_entry("rollout", task, n, res["kernel_us"], RING),
+                      "kernel_us_source": "HIP events on the step stream around the timed region / steps",
+                      "kernel_us_back_to_back": round(us_b2b, 3)}}
+    if "per_step" in res:
+        ps = res["per_step"]
+        e["per_step_launch"] = {"value": round(ps["value"], 1), "ms_per_step": round(ps["ms_per_step"], 5),
+                                "roofline": {**roofline_entry("step", task, n, ps["kernel_us"]),
+                                             "kernel_us_back_to_back": round(us_b2b_step, 3)}}
+    if sweep:
+        e["roofline_sweep"] = sweep
+    return e
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:   # forked workers: before anything initialises the GPU
+        cpu = cpu_baseline_leg(args.task, args.num_envs, args.seed, args.cpu_seconds)
+
+    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env
+    rank, world, local = init_from_env()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # one GPU per rank (torchrun's LOCAL_RANK); modulo the device count so an N-rank rehearsal with
+    # OUZ_DIST_BACKEND=gloo can share one GPU
+    n_dev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local % n_dev)
+    torch.cuda.set_device(dev)
+    n = args.num_envs
+
+    # per-rollout return statistics all-reduced (RCCL when N > 1) asynchronously on the collective's
+    # stream, double-buffered so the next rollouts' steps do not wait for it, and ARB rollouts' rows per
+    # collective: one dist.all_reduce call costs ~20 us of host time (distributed.ReturnAllReduce)
+    red = ReturnAllReduce(dev, batch=args.allreduce_batch)
+    run, res = measure(args.task, n, dev, args.seed, rank, world, args, red)
 
     if rank != 0:
         if world > 1:
@@ -248,44 +373,54 @@ def main():
             dist.destroy_process_group()
         return
 
-    us_b2b = kernel_time_us(env, ring)
-    us = ev["steps"]
+    letter = TASK_CONFIG.get(args.task, "-")
+    desc = CONFIGS[letter][2] if letter in CONFIGS else args.task
+    us_b2b = run.back_to_back_us(fused=True)
+    us_b2b_step = run.back_to_back_us(fused=False)
+    ps = res["per_step"]
+    backend = dist.get_backend() if world > 1 else None
     out = {
-        "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"config B: {n}-env x500 hover, Lee position controller ({args.task}), fp32, "
-                               "dt 0.01 x 2 sub-steps",
+        "metric": METRIC, "value": round(res["value"], 1), "unit": "env-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"config {letter}: {n}-env {desc} ({args.task}), dt 0.01 x 2 sub-steps; "
+                               f"16-step rollouts, one persistent launch each (ouz_rollout_stats)",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
                    "parallelism": f"env-sharded dp{world} (per-16-step-rollout return statistics, async RCCL "
-                                  f"all-reduce of {args.allreduce_batch} rollouts' rows per collective)"},
-        "roofline": {**roofline_entry(args.task, n, us),
+                                  f"all-reduce of {args.allreduce_batch} rollouts' rows per collective)",
+                   "physical_devices": min(world, n_dev), "backend": backend,
+                   "rehearsal": bool(world > 1 and (backend != "nccl" or n_dev < world))},
+        "roofline": {**roofline_entry("rollout", args.task, n, res["kernel_us"], RING),
                      "kernel_us_source": "HIP events on the step stream around the timed region / steps "
-                                         "(includes the per-rollout episode statistics)",
+                                         "(16-step rollout launches, episode statistics fused)",
                      "kernel_us_back_to_back": round(us_b2b, 3),
                      "regime": "latency-bound: 4096 envs' state is L2/MALL-resident, see roofline_sweep"},
-        "python_vectask_step_rate": round(py_rate, 1) if py_rate else None,
+        "per_step_launch": {
+            "value": round(ps["value"], 1), "ms_per_step": round(ps["ms_per_step"], 5),
+            "note": "the same steps as one quad_step_kernel launch per VecTask.step (ouz_step_n_stats: one C "
+                    "call per 16-step rollout, episode statistics as a separate launch)",
+            "roofline": {**roofline_entry("step", args.task, n, ps["kernel_us"]),
+                         "kernel_us_back_to_back": round(us_b2b_step, 3)}},
     }
-    if value_fused is not None:
-        out["fused_rollout"] = {"value": round(value_fused, 1), "unit": "env-steps/s",
-                                "ms_per_step": round(el_fused / args.steps * 1e3, 5),
-                                "kernel_us_per_step": round(kernel_time_us(env, ring, 320, fused=True), 3),
-                                "note": "ouz_rollout: 16 steps per launch into (16, N, ...) rollout storage, env "
-                                        "state in registers; same steps, same per-step outputs"}
-    if world == 1 and not args.no_sweep:
-        sweep = []
-        del env
+    if world == 1:
+        del run
         torch.cuda.empty_cache()
-        for big in [int(x) for x in args.sweep.split(",") if x]:
-            e2 = make_env(args.task, big, dev, args.seed, 0, big)
-            r2 = action_ring(big, dev, args.seed)[:2].contiguous()
-            e2.rollout(r2, 20)
-            sweep.append(roofline_entry(args.task, big, kernel_time_us(e2, r2, reps=50)))
-            del e2, r2
-            torch.cuda.empty_cache()
-        out["roofline_sweep"] = sweep
-    if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.task, n, args.seed, args.cpu_seconds)
+        if not args.no_sweep:
+            out["roofline_sweep"] = sweep_entries(args.task, [int(x) for x in args.sweep.split(",") if x],
+                                                  dev, args.seed)
+        if not args.no_configs:
+            cfgs = []
+            for L, (task, cn, _) in CONFIGS.items():
+                if task == args.task:
+                    continue
+                r2, res2 = measure(task, cn, dev, args.seed, 0, 1, args, ReturnAllReduce(dev, batch=1))
+                sw = None if args.no_sweep else sweep_entries(task, [1 << 22], dev, args.seed)
+                cfgs.append(config_entry(L, task, cn, res2, r2, sw))
+                del r2
+                torch.cuda.empty_cache()
+            out["configs"] = cfgs
+        if cpu is not None:
+            out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

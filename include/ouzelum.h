@@ -26,6 +26,10 @@
  *                   (the learners' obs[step] = next_obs buffers, PPO/main.py:67-73,88-96) or to the
  *                   env buffers.  For the Lee tasks actions are ignored (ekf_lee_landed.py:308), so a
  *                   fused rollout is exactly K VecTask.step calls.
+ *   ouz_pre_physics the task's pre_physics_step alone (ekf_lee_landed.py:308-530, lee_landed.py:263-330,
+ *                   ouzelum.py:218-251): lazy reset, estimator / controller / guidance / thrust model, and the
+ *                   body wrench handed to apply_rigid_body_force_tensors; no integration, no outputs, the
+ *                   step counter does not advance (a component entry for parity tests, not half a step)
  *   ouz_reset_idx   VecTask.reset_idx / reset_done (lazy: marks reset_buf)
  *                                              tasks/base/vec_task.py:369-406, ekf_lee_landed.py:271-306
  *   ouz_lee_control Controller.__call__        controllers/controller.py:45-48 (+ position/velocity/attitude)
@@ -204,6 +208,17 @@ int ouz_step(ouz_env* env, const float* actions, void* stream);
 int ouz_step_n(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, void* stream);
 int ouz_rollout(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, float* obs_out,
                 float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, void* stream);
+/* ouz_rollout followed by the rollout's episode statistics (as ouz_episode_stats would write them),
+ * reduced inside the last rollout launch: one launch per rollout of <= 32 steps, no statistics kernel
+ * (RPO-LSTM/main.py:96-110: T env steps, then RecordEpisodeStatisticsTorch's returns). */
+int ouz_rollout_stats(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, float* obs_out,
+                      float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int32_t drain,
+                      void* stream);
+/* pre_physics_step of the next step on the env state (see the table above): wrench [num_envs][6] f32 gets
+ * (force xyz, torque xyz) in the body frame at the COM -- the lumped form of the forces / torques the
+ * reference passes to gym.apply_rigid_body_force_tensors (LOCAL_SPACE).  reset_buf is cleared for the
+ * envs it reset (reset_idx, ekf_lee_landed.py:300-301); obs / rew / time_outs are not written. */
+int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* stream);
 int ouz_reset_idx(ouz_env* env, const int32_t* env_ids, int32_t n, void* stream);
 int ouz_reset_all(ouz_env* env, void* stream);
 /* Episode statistics of envs created with track_episodes: writes the f64 triple

@@ -805,6 +805,7 @@ class OracleEnv:
             else:
                 self._pre_lee_est(m, spec, rst, t, f_b, tau_b)
 
+        self.last_f_b, self.last_tau_b = f_b.copy(), tau_b.copy()   # the wrench gym.simulate integrates
         # ---- physics (vec_task.py:332-335 -> build-defined integrator) ----
         mass = MASS * self.dr[:, 0]
         inertia = INERTIA[None, :] * self.dr[:, 1:2]

@@ -93,6 +93,8 @@ SIGNATURES = {
     "ouz_step": (_I, [_P, _P, _P]),
     "ouz_step_n": (_I, [_P, _P, _I, _I, _P]),
     "ouz_rollout": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P]),
+    "ouz_rollout_stats": (_I, [_P, _P, _I, _I, _P, _P, _P, _P, _P, _I, _P]),
+    "ouz_pre_physics": (_I, [_P, _P, _P, _P]),
     "ouz_reset_idx": (_I, [_P, _P, _I, _P]),
     "ouz_reset_all": (_I, [_P, _P]),
     "ouz_episode_stats": (_I, [_P, _P, _I, _P]),

@@ -489,9 +489,12 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
 // ---------------------------------------------------------------------------
 // One VecTask.step of one env on register state (mirrors oracle/quad_oracle.py::OracleEnv.step)
 // ---------------------------------------------------------------------------
-template <int CTRL, int TGT>
+// PRE: pre_physics_step only (ouz_pre_physics) -- stop before the integrator and write the body wrench
+// [6] (force, torque; body frame at the COM) that gym.simulate would integrate to `wrench`.
+template <int CTRL, int TGT, bool PRE = false>
 __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
-                                         EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout) {
+                                         EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout,
+                                         float* wrench = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const EnvConsts& c = a.c;
   const bool rst = S.rst;
@@ -682,6 +685,12 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     tau_b = tau;
   }
 
+  if constexpr (PRE) {
+    float* wr = wrench + (size_t)i * 6;
+    wr[0] = f_b.x; wr[1] = f_b.y; wr[2] = f_b.z;
+    wr[3] = tau_b.x; wr[4] = tau_b.y; wr[5] = tau_b.z;
+    return;
+  }
   OUZ_STAMP(3, false);
   // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
   {
@@ -842,10 +851,16 @@ __device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bo
 
 // K steps of one env: load once, K x (step + emit), store once.  MULTI = false is the single
 // VecTask.step kernel (K = 1, no loop, no rollout storage) and keeps the register budget of one step.
-template <int CTRL, int TGT, bool MULTI>
+// Episode statistics of one lane, reduced over the grid by the fused rollout (RolloutStats).
+struct LaneStats {
+  double sum, cnt, len;
+};
+
+template <int CTRL, int TGT, bool MULTI, bool PRE = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, bool valid, int task,
-                                        bool direct = false) {
+                                        bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
+                                        float* wrench = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const uint32_t gid = a.env_offset + (uint32_t)i;
   EnvRegs<CTRL, TGT> S;
@@ -853,8 +868,25 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
   if (valid) env_load<CTRL, TGT>(a, i, tp, S, ctx[0].actions);
+  // fused statistics: the episode accumulators of earlier (unfused) steps, in flight with the state
+  float ep_sum_old = 0.0f;
+  int32_t ep_cnt_old = 0, ep_len_old = 0;
+  if (MULTI && stats_mode && valid) {
+    ep_sum_old = ld(S.T, OUZ_F_EP_SUM);
+    ep_cnt_old = ldi(S.T, OUZ_I_EP_CNT);
+    ep_len_old = ldi(S.T, OUZ_I_EP_LEN);
+  }
   OUZ_STAMP(1, true);
-  if constexpr (!MULTI) {
+  if constexpr (PRE) {
+    // pre_physics_step alone: lazy reset, controller / estimator / guidance, wrench; reset_idx clears
+    // reset_buf (ekf_lee_landed.py:300-301); no integration, no outputs, the step counter stays
+    float ob[OUZ_NUM_OBS];
+    float rew = 0.0f;
+    bool rs = false, to = false;
+    const bool did_reset = valid && S.rst;
+    if (valid) env_core<CTRL, TGT, true>(a, ctx[0], i, gid, task, S, ob, rew, rs, to, wrench);
+    if (did_reset) a.reset[i] = 0;
+  } else if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
@@ -892,6 +924,28 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
         emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
       }
     }
+    if (stats_mode && valid) {
+      // RecordEpisodeStatisticsTorch over the rollout (PPO/utils.py:20-35) without a separate launch: this
+      // lane's totals (accumulated before + finished in these K steps, same f32 adds as the atomics of
+      // env_store) go to the grid reduction; drained accumulators are zeroed, kept ones written back.
+      const float s_tot = ep_sum_old + S.ep_sum_add;
+      const int32_t c_tot = ep_cnt_old + S.ep_cnt_add, l_tot = ep_len_old + S.ep_len_add;
+      ls->sum += (double)s_tot;
+      ls->cnt += (double)c_tot;
+      ls->len += (double)l_tot;
+      if (stats_mode == 2) {
+        if (ep_cnt_old) {
+          st(S.T, OUZ_F_EP_SUM, 0.0f);
+          sti(S.T, OUZ_I_EP_CNT, 0);
+          sti(S.T, OUZ_I_EP_LEN, 0);
+        }
+      } else if (S.ep_cnt_add) {
+        st(S.T, OUZ_F_EP_SUM, s_tot);
+        sti(S.T, OUZ_I_EP_CNT, c_tot);
+        sti(S.T, OUZ_I_EP_LEN, l_tot);
+      }
+      S.ep_cnt_add = 0;   // env_store: no accumulator atomics
+    }
   }
   if (valid) env_store<CTRL, TGT>(a, i, tp, S);
   OUZ_STAMP(7, true);
@@ -900,10 +954,21 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
 
 constexpr int kMaxRolloutChunk = 32;
 
+// Episode statistics fused into the last launch of a rollout (ouz_rollout_stats): each wave reduces its
+// lanes' totals into partials[wave]; the last wave to finish (device-scope ticket) adds the partials in
+// wave order, so the triple is deterministic.  mode 0: off, 1: report, 2: report and drain.
+struct RolloutStats {
+  double* out;
+  double* partials;         // [tiles][3]
+  uint32_t* ticket;         // returns to 0 after every launch
+  int32_t mode;
+};
+
 struct RolloutArgs {
   int32_t K;
   OutPtrs outs[2];          // [0] per-step target (env buffers or rollout storage), [1] env buffers
   uint64_t out_stride;      // 0: write every step to outs[0]; else rollout storage with this env stride
+  RolloutStats stats;
   StepCtx ctx[kMaxRolloutChunk];
 };
 
@@ -932,23 +997,63 @@ __device__ __forceinline__ void prefetch_kernargs() {
 }
 
 // The step kernel body: one env per lane, K steps (MULTI) or one.
-template <int TASK, bool MULTI>
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Grid reduction of the lanes' episode statistics (see RolloutStats).  Called once per live wave.
+__device__ __forceinline__ void reduce_stats(const RolloutStats& rs, int n, int first, const LaneStats& ls) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t w = (uint32_t)first >> 6, nw = (uint32_t)(n + 63) >> 6;
+  const double s = wave_sum(ls.sum), c = wave_sum(ls.cnt), l = wave_sum(ls.len);
+  uint32_t last = 0;
+  if (lane == 0u) {
+    rs.partials[w * 3u + 0u] = s;
+    rs.partials[w * 3u + 1u] = c;
+    rs.partials[w * 3u + 2u] = l;
+    __threadfence();
+    last = atomicAdd(rs.ticket, 1u) == nw - 1u ? 1u : 0u;
+  }
+  last = __shfl(last, 0, 64);
+  if (!last) return;
+  __threadfence();
+  double t[3] = {0.0, 0.0, 0.0};
+  for (uint32_t j = lane; j < nw; j += 64u) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) t[k] += __builtin_nontemporal_load(&rs.partials[j * 3u + (uint32_t)k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) t[k] = wave_sum(t[k]);
+  if (lane == 0u) {
+    rs.out[0] = t[0];
+    rs.out[1] = t[1];
+    rs.out[2] = t[2];
+    *rs.ticket = 0u;   // ready for the next launch
+  }
+}
+
+template <int TASK, bool MULTI, bool PRE = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
-                                          uint64_t out_stride) {
+                                          uint64_t out_stride, const RolloutStats* rst = nullptr,
+                                          float* wrench = nullptr) {
   __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
   const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;
   const int first = i - (int)(threadIdx.x & 63);
   if (first >= a.n) return;                 // whole wave past the end
   const bool valid = i < a.n;
+  const int sm = (MULTI && rst) ? rst->mode : 0;
+  LaneStats ls{0.0, 0.0, 0.0};
   if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-    run_env<CTRL_RL, TGT_GOAL, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK);
+    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -958,15 +1063,16 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     const bool vl = valid && t == OUZ_TASK_LEE_LANDED, vt = valid && t == OUZ_TASK_TRACKING;
     const bool vr = valid && !vl && !vt;
     if (__any(vl))
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vl,
-                                                  OUZ_TASK_LEE_LANDED, direct);
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vl,
+                                                  OUZ_TASK_LEE_LANDED, direct, sm, &ls, wrench);
     if (__any(vt))
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vt,
-                                             OUZ_TASK_TRACKING, direct);
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vt,
+                                             OUZ_TASK_TRACKING, direct, sm, &ls, wrench);
     if (__any(vr))
-      run_env<CTRL_RL, TGT_GOAL, MULTI>(a, ctx, K, outs, out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
-                                        direct);
+      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
+                                        direct, sm, &ls, wrench);
   }
+  if (sm) reduce_stats(*rst, a.n, first, ls);
 }
 
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
@@ -979,11 +1085,18 @@ __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCt
   step_body<TASK, false>(a, &c, 1, env_out, 0);
 }
 
+// ouz_pre_physics: pre_physics_step alone, the body wrench to `wrench` [n][6].
+template <int TASK>
+__global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx c, float* wrench) {
+  const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
+  step_body<TASK, false, true>(a, &c, 1, env_out, 0, nullptr, wrench);
+}
+
 // ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.
 template <int TASK>
 __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true>(a, r.ctx, r.K, r.outs, r.out_stride);
+  step_body<TASK, true>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
@@ -1033,11 +1146,6 @@ __global__ void mark_all_kernel(int64_t* reset, int32_t n) {
 constexpr int kStatsBlock = 256;
 constexpr int kStatsMaxBlocks = 256;
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 
 __global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, double* partials, uint32_t* ticket,
                                                                     double* out, int drain) {
@@ -1300,6 +1408,8 @@ struct ouz_env {
   ouz_dr_noise* drn_dev;     // [2] DR noise params (read by the step kernel only when enabled)
   ouz_dr_noise drn_host[2];
   uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
+  double* wave_partials;     // [tiles][3] per-wave partials of the fused rollout statistics
+  uint32_t* wave_ticket;     // their last-wave counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
 };
 
@@ -1391,6 +1501,13 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
   r = hip_check(hipMalloc(&e->drn_dev, 2 * sizeof(ouz_dr_noise)), "hipMalloc(dr noise)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
+  const size_t n_tiles = (size_t)OUZ_TILES(cfg->num_envs);
+  r = hip_check(hipMalloc(&e->wave_partials, n_tiles * 3 * sizeof(double) + 64), "hipMalloc(wave partials)");
+  if (r) { (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
+  e->wave_ticket = reinterpret_cast<uint32_t*>(e->wave_partials + n_tiles * 3);
+  r = hip_check(hipMemset(e->wave_ticket, 0, sizeof(uint32_t)), "hipMemset(wave ticket)");
+  if (r) { (void)hipFree(e->wave_partials); (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials);
+           (void)hipFree(e->wp_tab); delete e; return r; }
   std::memset(e->drn_host, 0, sizeof(e->drn_host));
   r = hip_check(hipMemset(e->stats_ticket, 0, sizeof(uint32_t)), "hipMemset(stats)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
@@ -1441,6 +1558,7 @@ int ouz_destroy(ouz_env* env) {
   if (env->wp_tab) (void)hipFree(env->wp_tab);
   if (env->stats_partials) (void)hipFree(env->stats_partials);
   if (env->drn_dev) (void)hipFree(env->drn_dev);
+  if (env->wave_partials) (void)hipFree(env->wave_partials);
   delete env;
   return OUZ_OK;
 }
@@ -1494,12 +1612,13 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
 // ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
 // storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
 static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64_t ring_pos, int32_t K,
-                        const OutPtrs* storage, hipStream_t s) {
+                        const OutPtrs* storage, hipStream_t s, double* stats_out = nullptr, int stats_mode = 0) {
   const StepArgs& a = env->args;
   const int n = env->cfg.num_envs, blk = block_for(n);
   RolloutArgs r;
   std::memset(&r, 0, sizeof(r));
   r.K = K;
+  if (stats_mode) r.stats = RolloutStats{stats_out, env->wave_partials, env->wave_ticket, stats_mode};
   const OutPtrs envout{env->buf.obs, env->buf.rew, env->buf.reset, env->buf.timeouts};
   r.outs[0] = storage ? *storage : envout;
   r.outs[1] = envout;
@@ -1513,7 +1632,7 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
   dim3 g(grid_for(n, blk)), b(blk);
 #define OUZ_LAUNCH_TASK(T)                                         \
   do {                                                             \
-    if (K == 1 && !storage) {                                      \
+    if (K == 1 && !storage && !stats_mode) {                       \
       hipLaunchKernelGGL(quad_step_kernel<T>, g, b, 0, s, a, r.ctx[0]); \
     } else {                                                       \
       hipLaunchKernelGGL(quad_rollout_kernel<T>, g, b, 0, s, a, r); \
@@ -1559,21 +1678,63 @@ int ouz_step_n(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_step
   return OUZ_OK;
 }
 
-int ouz_rollout(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out, float* rew_out,
-                int64_t* reset_out, uint8_t* timeouts_out, void* stream) {
-  int rc = check_ring(env, ring, ring_len, n_steps, "ouz_rollout");
+static int rollout_impl(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out,
+                        float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int stats_mode,
+                        void* stream, const char* fn) {
+  int rc = check_ring(env, ring, ring_len, n_steps, fn);
   if (rc) return rc;
   const bool store = obs_out || rew_out || reset_out || timeouts_out;
   if (store && !(obs_out && rew_out && reset_out && timeouts_out))
-    return fail(OUZ_ERR_INVALID, "ouz_rollout: give all four storage pointers or none");
+    return fail(OUZ_ERR_INVALID, std::string(fn) + ": give all four storage pointers or none");
   const size_t n = (size_t)env->cfg.num_envs;
   for (int32_t k0 = 0; k0 < n_steps; k0 += kMaxRolloutChunk) {
     const int32_t K = (n_steps - k0) < kMaxRolloutChunk ? (n_steps - k0) : kMaxRolloutChunk;
     OutPtrs st{obs_out + (size_t)k0 * n * OUZ_NUM_OBS, rew_out + (size_t)k0 * n, reset_out + (size_t)k0 * n,
                timeouts_out + (size_t)k0 * n};
-    rc = launch_steps(env, ring, ring_len, k0, K, store ? &st : nullptr, (hipStream_t)stream);
+    const bool last = k0 + K >= n_steps;
+    rc = launch_steps(env, ring, ring_len, k0, K, store ? &st : nullptr, (hipStream_t)stream, stats_out,
+                      last ? stats_mode : 0);
     if (rc) return rc;
   }
+  return OUZ_OK;
+}
+
+int ouz_rollout(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out, float* rew_out,
+                int64_t* reset_out, uint8_t* timeouts_out, void* stream) {
+  return rollout_impl(env, ring, ring_len, n_steps, obs_out, rew_out, reset_out, timeouts_out, nullptr, 0, stream,
+                      "ouz_rollout");
+}
+
+int ouz_rollout_stats(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out,
+                      float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int32_t drain,
+                      void* stream) {
+  if (!stats_out) return fail(OUZ_ERR_INVALID, "ouz_rollout_stats: null stats_out");
+  if (env && !env->cfg.track_episodes)
+    return fail(OUZ_ERR_INVALID, "ouz_rollout_stats: env created without track_episodes");
+  if (n_steps <= 0) return fail(OUZ_ERR_INVALID, "ouz_rollout_stats: n_steps must be > 0");
+  return rollout_impl(env, ring, ring_len, n_steps, obs_out, rew_out, reset_out, timeouts_out, stats_out,
+                      drain ? 2 : 1, stream, "ouz_rollout_stats");
+}
+
+int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* stream) {
+  int rc = check_ring(env, actions, 1, 1, "ouz_pre_physics");
+  if (rc) return rc;
+  if (!wrench) return fail(OUZ_ERR_INVALID, "ouz_pre_physics: null wrench");
+  const StepArgs& a = env->args;
+  const int n = env->cfg.num_envs, blk = block_for(n);
+  StepCtx c{(uint32_t)env->step, flicker_mask(a, env->cfg.task, (uint32_t)env->step), actions};
+  dim3 g(grid_for(n, blk)), b(blk);
+  hipStream_t s = (hipStream_t)stream;
+  switch (env->cfg.task) {
+    case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a, c, wrench); break;
+    case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
+    case OUZ_TASK_EKF_LEE_LANDED:
+      hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
+    case OUZ_TASK_TRACKING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_TRACKING>, g, b, 0, s, a, c, wrench); break;
+    case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
+    default: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a, c, wrench); break;
+  }
+  OUZ_LAUNCH_CHECK("quad_pre_kernel");
   return OUZ_OK;
 }
 

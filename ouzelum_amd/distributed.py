@@ -71,6 +71,7 @@ class ReturnAllReduce:
         self.lo = [0] * depth       # first row of the block not yet in a submitted collective
         self.filled = [0] * depth   # rows of the block submitted by the caller
         self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        self._base = None
 
     def _where(self, r):
         return (r // self.batch) % self.depth, r % self.batch
@@ -93,6 +94,16 @@ class ReturnAllReduce:
             self._wait(d)
             self.lo[d] = self.filled[d] = 0
         return self.slots[d, row]
+
+    def slot_ptr(self, r):
+        """Device address of ``slot(r)`` (the same waiting), for C entry points that take a double*."""
+        d, row = self._where(r)
+        if row == 0:
+            self._wait(d)
+            self.lo[d] = self.filled[d] = 0
+        if self._base is None:
+            self._base = self.slots.data_ptr()
+        return self._base + (d * self.batch + row) * self.slots.shape[2] * 8
 
     def submit(self, r):
         d, row = self._where(r)

@@ -174,6 +174,42 @@ class QuadVecTask:
         t = self.istate[:, f0:f1, :].permute(1, 0, 2).reshape(f1 - f0, -1)
         return t[:, :self.num_envs]
 
+    def set_frows(self, f0, values):
+        """Write float fields [f0, f0 + k) of every env from a (k, N) tensor / array (the tiled counterpart of
+        gym.set_actor_root_state_tensor_indexed / set_dof_state_tensor, ekf_lee_landed.py:288,335)."""
+        self._set_rows(self.fstate, f0, values, torch.float32)
+
+    def set_irows(self, f0, values):
+        """Write int32 fields [f0, f0 + k) of every env from a (k, N) tensor / array."""
+        self._set_rows(self.istate, f0, values, torch.int32)
+
+    def _set_rows(self, buf, f0, values, dtype):
+        v = torch.as_tensor(values, dtype=dtype, device=self.device)
+        if v.dim() == 1:
+            v = v[None]
+        k, n = v.shape
+        if n != self.num_envs or f0 < 0 or f0 + k > buf.shape[1]:
+            raise ValueError(f"rows [{f0}, {f0 + k}) x {n} do not fit fields of {self.num_envs} envs")
+        pad = torch.zeros((k, buf.shape[0] * L.TILE), dtype=dtype, device=self.device)
+        pad[:, :n] = v
+        buf[:, f0:f0 + k, :] = pad.reshape(k, buf.shape[0], L.TILE).permute(1, 0, 2)
+
+    def set_root_states(self, root13):
+        """(N, 13) [p, q_xyzw, v, w] into the env state (the reference writes root_states in place and pushes
+        them with set_actor_root_state_tensor_indexed, ekf_lee_landed.py:335)."""
+        r = torch.as_tensor(root13, dtype=torch.float32, device=self.device)
+        self.set_frows(0, r.t())
+
+    def pre_physics(self, actions=None):
+        """The task's pre_physics_step alone (``ouz_pre_physics``): lazy reset, estimator / controller /
+        guidance / thrust model applied to the env state, and the (N, 6) body wrench (force, torque in the
+        body frame) the reference hands to gym.apply_rigid_body_force_tensors.  The step counter does not
+        advance and nothing is integrated -- a component entry for parity tests, not half a step."""
+        wrench = torch.empty((self.num_envs, 6), dtype=torch.float32, device=self.device)
+        L.check(L.lib.ouz_pre_physics(self._env, self._actions_ptr(actions), L.ptr(wrench), self._stream()),
+                "ouz_pre_physics")
+        return wrench
+
     @property
     def progress_buf(self):
         """progress_buf (int32; the reference keeps int64).  A snapshot copy."""
@@ -371,9 +407,52 @@ class QuadVecTask:
                 if tuple(tns.shape[:len(shape)]) != shape or tns.dtype != dt:
                     raise ValueError(f"storage {name} must be {shape} {dt}")
             ptrs = [L.ptr(obs), L.ptr(rew), L.ptr(rst), L.ptr(to)]
-        L.check(L.lib.ouz_rollout(self._env, ring_ptr, ring_len, int(n_steps), *ptrs, self._stream()), "ouz_rollout")
-        if stats_out is not None:
-            self.episode_stats(drain, out=stats_out)
+        if stats_out is not None:   # statistics reduced inside the last rollout launch
+            L.check(L.lib.ouz_rollout_stats(self._env, ring_ptr, ring_len, int(n_steps), *ptrs, L.ptr(stats_out),
+                                            1 if drain else 0, self._stream()), "ouz_rollout_stats")
+        else:
+            L.check(L.lib.ouz_rollout(self._env, ring_ptr, ring_len, int(n_steps), *ptrs, self._stream()),
+                    "ouz_rollout")
+
+    def rollout_plan(self, action_ring, n_steps, storage=None, drain=True):
+        """A validated, pre-bound form of ``rollout(action_ring, n_steps, fused=True, storage, stats_out, drain)``
+        for a loop that repeats the same rollout shape: returns ``run(stats_out_ptr)``, one C call
+        (``ouz_rollout_stats``: the K steps fused into one launch per 32 steps with the episode statistics
+        reduced in the last one) and no per-call checks.  ``stats_out_ptr`` is the device address of a
+        contiguous float64 tensor of >= 3 on this device (e.g. a ``ReturnAllReduce`` slot).  The caller keeps
+        ``action_ring`` and ``storage`` alive while the plan is used."""
+        if not self.cfg.track_episodes:
+            raise RuntimeError("create the env with track_episodes=True")
+        n_steps = int(n_steps)
+        if n_steps <= 0:
+            raise ValueError("n_steps must be > 0")
+        if action_ring is None:
+            ring_ptr, ring_len = (L.ptr(self._zero_actions) if self.uses_actions else None), 1
+        else:
+            L.require_hip_tensor(action_ring, "action_ring")
+            if action_ring.dim() != 3 or action_ring.shape[1:] != (self.num_envs, self.num_actions):
+                raise ValueError("action_ring must be (T, num_envs, 4)")
+            if action_ring.dtype != torch.float32 or not action_ring.is_contiguous():
+                raise ValueError("action_ring must be contiguous float32")
+            ring_ptr, ring_len = L.ptr(action_ring), action_ring.shape[0]
+        ptrs = [None] * 4
+        if storage is not None:
+            n = self.num_envs
+            for tns, shape, dt, name in ((storage[0], (n_steps, n, 13), torch.float32, "obs"),
+                                         (storage[1], (n_steps, n), torch.float32, "rew"),
+                                         (storage[2], (n_steps, n), torch.int64, "reset"),
+                                         (storage[3], (n_steps, n), torch.bool, "time_outs")):
+                L.require_hip_tensor(tns, name)
+                if tuple(tns.shape[:len(shape)]) != shape or tns.dtype != dt:
+                    raise ValueError(f"storage {name} must be {shape} {dt}")
+            ptrs = [L.ptr(t) for t in storage]
+        fn, env, stream, dr = L.lib.ouz_rollout_stats, self._env, self._stream(), 1 if drain else 0
+
+        def run(stats_out_ptr):
+            rc = fn(env, ring_ptr, ring_len, n_steps, ptrs[0], ptrs[1], ptrs[2], ptrs[3], stats_out_ptr, dr, stream)
+            if rc:
+                L.check(rc, "ouz_rollout_stats")
+        return run
 
     def reset(self):
         """vec_task.py:377-389: returns the current obs, does not touch the simulation."""

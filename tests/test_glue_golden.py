@@ -1,0 +1,123 @@
+"""The oracle's task glue against the REFERENCE's own task code (tests/golden/glue_*.npz).
+
+The fixtures were written by tests/golden/make_glue_golden.py, which runs the reference's VecTask.step and
+the EKFLeeLanded / LeeLanded / Ouzelum task methods it calls (reset_idx, set_targets, pre_physics_step with
+the EKF / PV-filter loops and the Lee controller, post_physics_step, compute_observations, the jit reward)
+on stub isaacgym / gym modules, with gym.simulate replaced by the build's integrator and the random draws by
+the build's counter RNG.  Everything but the integrator is therefore pinned to the reference here: reset
+offsets (ekf_lee_landed.py:271-306), wrench modes and the global convergence window (:339,458-530), waypoint
+guidance (:464-492), the +9.8 accel alias (:345-368), the shared PV trigger counters (:425-440), estimate
+fusion (:494-501), observations (:653-665), reward / done / time-outs, random goals (ouzelum.py:180-233), the
+RL thrust model (ouzelum.py:235-251) and POMDPWrapper.observation (utils/POMDP.py:23-43).
+
+Deviations left, by name:
+* the angle-sensor flicker of EKFLeeLanded (ekf_lee_landed.py:383): when it fires the reference raises
+  (TypeError in ahrs_ekf.py:1335, recorded in glue_ekf_flicker.npz); the build feeds the zeroed measurement
+  to the filter.  Envs whose angle coin fires are excluded from that step's comparison.
+* the torch.cross dim bug of position_control.py:60 (wrong only when N == 3): no fixture has 3 envs.
+* LeeLanded's landing flag is one scalar for the whole batch (lee_landed.py:286-288); the build keeps one per
+  env.  It only feeds the landing counter, which is not compared.
+"""
+import numpy as np
+import pytest
+
+from oracle import quad_oracle as Q
+from tests import glue_helpers as G
+
+
+def _close(name, got, want, atol, rtol=0.0, mask=None):
+    got, want = np.asarray(got, np.float64), np.asarray(want, np.float64)
+    if mask is not None:
+        got, want = got[mask], want[mask]
+    err = np.abs(got - want) - (atol + rtol * np.abs(want))
+    if np.any(err > 0):
+        i = np.unravel_index(np.argmax(err), err.shape)
+        raise AssertionError(f"{name}: {got[i]!r} vs reference {want[i]!r} at {i}")
+
+
+# f64 oracle vs the f64 reference run: the only differences are the build's f32-rounded random offsets and
+# operation order
+TOL = {"p": 1e-6, "q": 1e-6, "v": 1e-6, "w": 1e-5, "obs": 1e-6, "rew": 1e-6, "target": 1e-6, "f_b": 2e-5,
+       "tau_b": 2e-5, "thrust": 1e-6, "ekf_q": 1e-6, "waypoint": 1e-6, "prev_v": 1e-6}
+
+
+def compare(name, o, fx, t, mask=None):
+    got = {"p": o.p, "q": o.q, "v": o.v, "w": o.w, "obs": o.obs, "rew": o.rew, "target": o.target,
+           "f_b": o.last_f_b, "tau_b": o.last_tau_b, "thrust": o.thrust}
+    if G.GLUE[name] == "EKFLeeLanded":
+        got.update({"ekf_q": G.quat_canon_wxyz(o.ekf_q), "waypoint": o.waypoint, "prev_v": o.prev_v})
+    for k, v in got.items():
+        want = G.quat_canon_wxyz(fx[k][t]) if k == "ekf_q" else fx[k][t]
+        _close(f"{name}@{t} {k}", v, want, TOL[k], 1e-7, mask)
+    if G.GLUE[name] == "EKFLeeLanded":
+        scale = np.maximum(1.0, np.abs(fx["pv_x"][t]).max(1, keepdims=True))
+        _close(f"{name}@{t} pv_x", o.pv_x / scale, fx["pv_x"][t] / scale, 1e-6, 0, mask)
+        pscale = np.abs(fx["pv_P"][t]).max((1, 2))[:, None, None]
+        _close(f"{name}@{t} pv_P", o.pv_P / pscale, fx["pv_P"][t] / pscale, 1e-6, 0, mask)
+        _close(f"{name}@{t} ekf_P", o.ekf_P, fx["ekf_P"][t], 1e-9, 1e-6, mask)
+    for k, v in (("reset", o.reset_buf), ("timeouts", o.timeouts), ("progress", o.progress)):
+        a, b = np.asarray(v).astype(np.int64), fx[k][t].astype(np.int64)
+        if mask is not None:
+            a, b = a[mask], b[mask]
+        np.testing.assert_array_equal(a, b, err_msg=f"{name}@{t} {k}")
+
+
+@pytest.mark.parametrize("name", ["ekf", "lee", "ouz"])
+def test_glue_free_run(name):
+    """The oracle started from the fixture's start state and stepped with its actions reproduces the reference's
+    whole trajectory (resets, time-outs, the convergence window, landings, random goals)."""
+    fx = G.load(name)
+    o = Q.OracleEnv(G.oracle_config(name, fx))
+    G.to_oracle(o, G.state(fx, -1, name))
+    for t in range(fx["p"].shape[0]):
+        o.step(fx["actions"][t])
+        compare(name, o, fx, t)
+
+
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz"])
+def test_glue_single_step(name):
+    """One oracle step from every recorded reference state (exclusions: see the module docstring)."""
+    fx = G.load(name)
+    n = fx["init_p"].shape[0]
+    for t in range(-1, fx["p"].shape[0] - 1):
+        o = Q.OracleEnv(G.oracle_config(name, fx))
+        G.to_oracle(o, G.state(fx, t, name))
+        o.step(fx["actions"][t + 1])
+        mask = ~fx["ekf_input_corrupted"][t + 1] if "ekf_input_corrupted" in fx else np.ones(n, bool)
+        compare(name, o, fx, t + 1, mask)
+
+
+def test_glue_fixtures_cover_the_branches():
+    """The trajectories cross what they are meant to pin."""
+    e, f, lee, ouz = G.load("ekf"), G.load("ekf_flicker"), G.load("lee"), G.load("ouz")
+    for fx in (e, f, lee, ouz):
+        # lazy resets at the first step and during the run; time-outs (progress >= max - 1) and deaths
+        assert fx["init_reset"].sum() >= 5 and fx["reset"][:-1].sum() >= 1 and fx["timeouts"].any()
+        assert fx["reset"].sum() > fx["timeouts"].sum() or fx is lee
+    assert int(e["convergence_time"]) < e["p"].shape[0]                 # crosses the global window
+    assert e["flag"].any()                                              # landing cut after the window
+    assert (np.abs(e["f_b"][:, :, 2]) < 1e-12).any() and (e["f_b"][int(e["convergence_time"]):, :, 2] > 0).any()
+    # whole-batch flicker fired on the obs / PV sites; angle coins were excluded on some envs only
+    assert (np.abs(f["obs"]).sum((1, 2)) == 0).any()
+    frac = f["ekf_input_corrupted"][int(f["convergence_time"]):].mean()
+    assert 0.05 < frac < 0.3
+    assert "unsupported operand" in str(f["ekf_input_corruption_error"])   # the reference's own TypeError
+    assert (np.abs(lee["obs"]).sum((1, 2)) == 0).any()                  # LeeLanded flicker fired
+    assert (ouz["progress"] % 500 == 0).any()                           # random goals redrawn
+    assert np.abs(ouz["thrust"]).max() > 0
+
+
+@pytest.mark.parametrize("mode", ["flicker", "random_noise", "flickering_and_random_noise"])
+def test_glue_pomdp_wrapper(mode):
+    """oracle.pomdp_apply == POMDPWrapper.observation (utils/POMDP.py:23-43) on the same coins and noise."""
+    fx = G.load("pomdp")
+    rows, seed, prob = int(fx["rows"]), int(fx["seed"]), float(fx[f"{mode}_prob"])
+    fired = 0
+    for call in range(fx[f"{mode}_x"].shape[0]):
+        x, y = fx[f"{mode}_x"][call], fx[f"{mode}_y"][call]
+        got = Q.pomdp_apply(x.astype(np.float32).astype(np.float64), Q.POMDP_NAMES[mode], prob, seed,
+                            np.arange(rows), call, 0, batch_tag=7)
+        np.testing.assert_allclose(got, y, rtol=1e-6, atol=1e-7)
+        fired += int(np.all(y == 0))
+    if mode != "random_noise":
+        assert 0 < fired < fx[f"{mode}_x"].shape[0], "the flicker coin should fire on some calls only"

@@ -311,6 +311,50 @@ def test_episode_stats_kernel(ouz, task, n):
     assert float(env.episode_stats()[1]) == 0.0          # drained
 
 
+@pytest.mark.parametrize("task,n,off", [("LeeLanded", 4096, 0), ("QuadFault", 70000, 0), ("Ouzelum", 1000, 0),
+                                        ("QuadMixed", 4096, 32), ("QuadTracking", 640, 0)])
+def test_rollout_stats_fused_matches_separate(ouz, task, n, off):
+    """ouz_rollout_stats (bench.py's headline launch: 16 fused steps with the episode statistics reduced in the
+    same launch by the last wave) == the same rollouts as ouz_rollout + ouz_episode_stats: identical trajectory
+    and rollout storage, identical episode counts / lengths, returns to f64 summation order; drained and
+    non-drained calls; 70000 envs exercise the 256-lane blocks, 1000 a ragged last wave, the misaligned mixed
+    shard the straddling waves."""
+    kw = dict(seed=21, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True,
+              env_id_offset=off, num_envs_total=off + n)
+    if task in ("QuadTracking", "QuadMixed"):
+        kw["convergence_time"] = 10
+    if task in ("LeeLanded", "QuadTracking"):
+        kw["max_episode_length"] = 40          # episodes finish inside the test
+    a, b = ouz.make(**kw), ouz.make(**kw)
+    g = torch.Generator(device="cuda").manual_seed(8)
+    ring = (torch.rand((16, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
+    st_a = (torch.empty((16, n, 13), device="cuda"), torch.empty((16, n), device="cuda"),
+            torch.empty((16, n), dtype=torch.int64, device="cuda"), torch.empty((16, n), dtype=torch.bool, device="cuda"))
+    st_b = tuple(torch.empty_like(x) for x in st_a)
+    plan = a.rollout_plan(ring, 16, storage=st_a)
+    plan_keep = a.rollout_plan(ring, 16, storage=st_a, drain=False)
+    total = 0.0
+    for r in range(7):
+        got = torch.full((3,), -1.0, dtype=torch.float64, device="cuda")
+        keep = r in (2, 3)
+        (plan_keep if keep else plan)(got.data_ptr())
+        b.rollout(ring, 16, fused=True, storage=st_b)
+        want = b.episode_stats(drain=not keep).clone()
+        torch.cuda.synchronize()
+        for x, y in zip(st_a, st_b):
+            assert torch.equal(x, y)
+        assert torch.equal(a.fstate, b.fstate) and torch.equal(a.istate, b.istate)
+        assert float(got[1]) == float(want[1]) and float(got[2]) == float(want[2])
+        torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-9)
+        total += float(got[1])
+    assert total > 0, "no episode finished: the test would not test anything"
+    # the rollout() entry with stats_out and fused=True takes the same path
+    s1 = torch.zeros(3, dtype=torch.float64, device="cuda")
+    a.rollout(ring, 5, fused=True, stats_out=s1)
+    b.rollout(ring, 5, fused=True)
+    torch.testing.assert_close(s1, b.episode_stats(), rtol=1e-12, atol=1e-9)
+
+
 def test_episode_stats_into_return_ring(ouz):
     """bench.py's per-rollout pattern: the rollout's statistics into ReturnAllReduce's double-buffered ring
     (rollout(stats_out=slot) or episode_stats(out=slot); single process: no collective) give the same
