@@ -128,7 +128,8 @@ def cpu_baseline_leg(task, n, seed, budget_s):
     head = next(r for r in table if r["task"] == task and r["num_envs"] == n)
     ref = C.reference_structure(n=16, budget_s=budget_s * 0.15)
     return {"value": head["value"], "unit": "env-steps/s", "cores": head["cores"], "kind": "port",
-            "sample": head["sample"] + f"; host {C.host_model()}, {cores} cores available (sched_getaffinity)",
+            "sample": head["sample"] + f"; host {C.host_model()}, {cores} cores available (affinity / cgroup quota "
+                                       "/ OMP_NUM_THREADS)",
             "host_cores": cores, "host_model": C.host_model(), "table": table,
             "reference_structure_estimator": {**ref, "config": "C"}}
 

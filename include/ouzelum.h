@@ -67,7 +67,9 @@ extern "C" {
 #define OUZ_TASK_TRACKING 3       /* EKF pipeline + trajectory platform + DR                    config C */
 #define OUZ_TASK_FAULT 4          /* RL thrust + single-rotor fault + obs noise                 config D */
 #define OUZ_TASK_MIXED 5          /* per-64-env curriculum of tasks 1/3/4                       config E */
-#define OUZ_NUM_TASKS 6
+#define OUZ_TASK_LANDING 6        /* RL thrust, land on the husky following its trajectories (tasks/landing.py);
+                                     the reference learners' default env (RPO-LSTM/main.py:18)              */
+#define OUZ_NUM_TASKS 7
 
 /* POMDP modes (utils/POMDP.py:5-20); -1 = task default */
 #define OUZ_POMDP_NONE 0

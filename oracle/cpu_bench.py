@@ -8,8 +8,8 @@ the product path, and nothing here touches the GPU.
 Two baselines:
 
 * ``vectorised``: the batched restatement on ALL host cores.  The envs of one
-  config are cut into contiguous shards, one per core (``os.sched_getaffinity``:
-  the box's CPU share, not the machine's core count); each worker process steps
+  config are cut into contiguous shards, one per core (``host_cores``: the box's
+  CPU share, not the machine's core count); each worker process steps
   its shard with its own ``OracleEnv`` (global env ids keep the shard's draws
   identical to the unsharded run) and all workers start timing at one barrier.
   Throughput = envs x steps / the slowest worker's time.  Workers are forked,
@@ -32,11 +32,42 @@ import time
 import numpy as np
 
 
-def host_cores() -> int:
+def _cgroup_cpus():
+    """CPU quota of this cgroup (cgroup v2 cpu.max, v1 cfs quota) in cores, or None when unlimited."""
     try:
-        return len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            return max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            quota = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            period = int(fh.read())
+        if quota > 0:
+            return max(1, quota // period)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def host_cores() -> int:
+    """The cores this process may use: the affinity mask, capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS (the GPU boxes give each one-GPU job a 16-core share of a larger machine through the
+    quota and set OMP_NUM_THREADS to it; the affinity mask there still lists every core)."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = _cgroup_cpus()
+    if q:
+        n = min(n, q)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def host_model() -> str:

@@ -599,9 +599,10 @@ def dr_noise_apply(x, p, seed, env_ids, step, stream):
 CTRL_RL, CTRL_LEE_TRUE, CTRL_LEE_EST = 0, 1, 2
 TGT_GOAL, TGT_PLATFORM, TGT_TRAJ = 0, 1, 2
 
-TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED = 0, 1, 2, 3, 4, 5
+TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 TASK_NAMES = {"Ouzelum": TASK_OUZELUM, "LeeLanded": TASK_LEE_LANDED, "EKFLeeLanded": TASK_EKF_LEE_LANDED,
-              "QuadTracking": TASK_TRACKING, "QuadFault": TASK_FAULT, "QuadMixed": TASK_MIXED}
+              "QuadTracking": TASK_TRACKING, "QuadFault": TASK_FAULT, "QuadMixed": TASK_MIXED,
+              "Landing": TASK_LANDING}
 MIXED_CHUNK = 64                       # envs per task block in the mixed curriculum (one wave)
 MIXED_TASKS = (TASK_LEE_LANDED, TASK_TRACKING, TASK_FAULT)
 
@@ -631,6 +632,8 @@ def task_spec(task, pomdp=None, pomdp_prob=None, max_episode_length=0):
         s = TaskSpec(CTRL_LEE_EST, TGT_PLATFORM, 700, 0.3, 0.25, False, -0.08, POMDP_FLICKER, 0.0)
     elif task == TASK_TRACKING:   # config C: EKF pipeline + kinematic trajectory platform + DR
         s = TaskSpec(CTRL_LEE_EST, TGT_TRAJ, 700, 0.3, 0.25, False, -0.08, POMDP_FLICKER, 0.0, dr=True)
+    elif task == TASK_LANDING:    # tasks/landing.py, cfg/task/Landing.yaml: RL thrust, husky on its trajectories
+        s = TaskSpec(CTRL_RL, TGT_TRAJ, 2000, 0.3, 0.0, False, 0.08)
     elif task == TASK_FAULT:      # config D: RL thrust + single-rotor fault + obs noise
         s = TaskSpec(CTRL_RL, TGT_GOAL, 2000, 0.5, 0.0, False, 0.0, POMDP_NOISE, 0.1,
                      fault=True, motor_yaw=True)
@@ -800,6 +803,8 @@ class OracleEnv:
             m = self.task_ids == task
             if spec.ctrl == CTRL_RL:
                 self._pre_rl(m, spec, a, rst, t, f_b, tau_b)
+                if spec.target_mode == TGT_TRAJ:        # set_husky_actions (landing.py:298,319-364)
+                    self._platform_step(m, t)
             elif spec.ctrl == CTRL_LEE_TRUE:
                 self._pre_lee_true(m, spec, rst, f_b, tau_b)
             else:
@@ -844,7 +849,7 @@ class OracleEnv:
     # -- RL thrust tasks (ouzelum.py:218-251) ---------------------------------
     def _pre_rl(self, m, spec, a, rst, t, f_b, tau_b):
         cfg = self.cfg
-        set_t = m & ((self.progress % 500 == 0) | rst)
+        set_t = m & ((self.progress % 500 == 0) | rst) & (spec.target_mode == TGT_GOAL)
         wt = rng.draw_u32(cfg.seed, self.gid, t, rng.RNG_TARGET)
         tx = (rng.u32_to_unit_f32(wt[0]) * np.float32(10) - np.float32(5)).astype(np.float32)
         ty = (rng.u32_to_unit_f32(wt[1]) * np.float32(10) - np.float32(5)).astype(np.float32)
@@ -984,6 +989,7 @@ class OracleEnv:
         cfg = self.cfg
         wp = self._traj_point(self.traj_idx)
         d = np.sqrt(((wp - self.plat) ** 2).sum(-1))
+        margin = np.abs(d - 0.2)                 # distance of this step's decisions from their thresholds
         adv = m & (d < 0.2)
         self.traj_idx[adv] += 1
         done = m & (self.traj_idx >= self._traj_len())
@@ -991,6 +997,10 @@ class OracleEnv:
             self._new_traj(done, t)
         wp = self._traj_point(self.traj_idx)
         lin, ang, _ = drive_command(self.plat, wp, self.plat_heading, max_wheel=cfg.plat_speed / WHEEL_RADIUS)
+        dth = map_to_pi(np.arctan2(wp[:, 1] - self.plat[:, 1], wp[:, 0] - self.plat[:, 0]) - map_to_pi(self.plat_heading))
+        margin = np.minimum(margin, np.abs(np.abs(dth) - DRIVE_ANG_THRESH))
+        self.plat_margin = np.where(m, margin, np.inf) if getattr(self, "plat_margin", None) is None \
+            else np.where(m, margin, self.plat_margin)
         th = map_to_pi(self.plat_heading + ang * cfg.dt)
         pv = np.stack([lin * np.cos(th), lin * np.sin(th)], 1)
         self.plat_heading[m] = th[m]

@@ -23,8 +23,8 @@ class OuzelumError(RuntimeError):
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
 ABI_VERSION = 1
-TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED = range(6)
-NUM_TASKS = 6
+TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
+NUM_TASKS = 7
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
 LEE_POSITION, LEE_VELOCITY, LEE_ATTITUDE = range(3)
 NUM_OBS, NUM_ACT = 13, 4

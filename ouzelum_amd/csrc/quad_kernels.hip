@@ -84,6 +84,9 @@ static TaskParams task_preset(int task) {
     case OUZ_TASK_FAULT:
       t = TaskParams{CTRL_RL, TGT_GOAL, 2000, OUZ_POMDP_NOISE, 0.5f, 0.0f, 0.0f, 0.1f, 1, 1, 0, 0, 1, 1};
       break;
+    case OUZ_TASK_LANDING:  // tasks/landing.py, cfg/task/Landing.yaml: RL thrust + husky on its trajectories
+      t = TaskParams{CTRL_RL, TGT_TRAJ, 2000, OUZ_POMDP_NONE, 0.3f, 0.0f, 0.08f, 0.0f, 1, 1, 0, 0, 0, 0};
+      break;
     default:
       break;
   }
@@ -169,7 +172,7 @@ __device__ __forceinline__ void pomdp_apply(float* x, const TaskParams& tp, int 
       const float p = (mode == OUZ_POMDP_FLICKER) ? tp.pomdp_prob : 0.1f;
       fire = unit_f32(draw(a.seed, gid, sc.step, RNG_POMDP + site, 0).x) <= p;
     } else {
-      fire = (sc.flick_mask >> (task * 8 + site)) & 1u;
+      fire = (sc.flick_mask >> (tp_slot(task) * 8 + site)) & 1u;
     }
     if (fire) {
 #pragma unroll
@@ -540,10 +543,12 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 
   if constexpr (CTRL == CTRL_RL) {
     // ---- RL per-rotor thrust model (ouzelum.py:218-251) ----
-    if ((S.progress % 500) == 0 || rst) {   // set_targets (ouzelum.py:180-190)
-      U4 r = draw(a.seed, gid, sc.step, RNG_TARGET);
-      target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
-                  __fadd_rn(unit_f32(r.z), 1.0f));
+    if constexpr (TGT == TGT_GOAL) {
+      if ((S.progress % 500) == 0 || rst) {   // set_targets (ouzelum.py:180-190)
+        U4 r = draw(a.seed, gid, sc.step, RNG_TARGET);
+        target = v3(__fsub_rn(__fmul_rn(unit_f32(r.x), 10.0f), 5.0f), __fsub_rn(__fmul_rn(unit_f32(r.y), 10.0f), 5.0f),
+                    __fadd_rn(unit_f32(r.z), 1.0f));
+      }
     }
     float av[4] = {S.act.x, S.act.y, S.act.z, S.act.w};
     if (a.drn_mask & 2) dr_noise_apply<4>(av, a.drn[1], a.seed, gid, sc.step, RNG_DRN_ACT);   // vec_task.py:323-325
@@ -1052,6 +1057,8 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
     run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+  } else if constexpr (TASK == OUZ_TASK_LANDING) {
+    run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
     run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
   } else {
@@ -1602,7 +1609,7 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
     const float p = tp.pomdp == OUZ_POMDP_FLICKER ? tp.pomdp_prob : 0.1f;
     for (uint32_t site = 0; site < 6; ++site) {
       U4 r = draw(a.seed, BATCH_ENV, step, RNG_POMDP + site, (uint32_t)t);
-      if (unit_f32(r.x) <= p) m |= 1u << (t * 8 + site);
+      if (unit_f32(r.x) <= p) m |= 1u << (tp_slot(t) * 8 + site);
     }
   }
   return m;
@@ -1644,6 +1651,7 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
     case OUZ_TASK_EKF_LEE_LANDED: OUZ_LAUNCH_TASK(OUZ_TASK_EKF_LEE_LANDED); break;
     case OUZ_TASK_TRACKING: OUZ_LAUNCH_TASK(OUZ_TASK_TRACKING); break;
     case OUZ_TASK_FAULT: OUZ_LAUNCH_TASK(OUZ_TASK_FAULT); break;
+    case OUZ_TASK_LANDING: OUZ_LAUNCH_TASK(OUZ_TASK_LANDING); break;
     default: OUZ_LAUNCH_TASK(OUZ_TASK_MIXED); break;
   }
 #undef OUZ_LAUNCH_TASK
@@ -1652,7 +1660,9 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
   return OUZ_OK;
 }
 
-static bool needs_actions(int task) { return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_MIXED; }
+static bool needs_actions(int task) {
+  return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_MIXED || task == OUZ_TASK_LANDING;
+}
 
 static int check_ring(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, const char* fn) {
   if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, std::string(fn) + ": env not bound");
@@ -1732,6 +1742,7 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
       hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_TRACKING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_TRACKING>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
+    case OUZ_TASK_LANDING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LANDING>, g, b, 0, s, a, c, wrench); break;
     default: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a, c, wrench); break;
   }
   OUZ_LAUNCH_CHECK("quad_pre_kernel");

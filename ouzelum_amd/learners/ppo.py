@@ -117,15 +117,16 @@ class PPOLearner:
     def initial_state(self):
         return self.actor.initial_state(self.num_envs, self.device) if self.recurrent else None
 
-    def act(self, state, lstm_state=None, done=None):
+    def act(self, state, lstm_state=None, done=None, alias=False):
         """``get_action`` for one rollout step, replayed from a hipGraph on the GPU (``GraphedPolicy``)
-        unless ``OUZ_GRAPH_POLICY=0``.  The outputs are the graph's static tensors, overwritten by
-        the next call: copy what must outlive it (the rollout loop stores them into its buffers)."""
+        unless ``OUZ_GRAPH_POLICY=0``.  Returns fresh tensors; ``alias=True`` returns the graph's static
+        output tensors instead, overwritten by the next call (the rollout loop copies them into its
+        buffers at once and passes the LSTM carry straight back)."""
         if self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "1") == "0":
             return self.get_action(state, lstm_state, done)
         if getattr(self, "_graphed", None) is None:
             self._graphed = GraphedPolicy(self)
-        return self._graphed(state, lstm_state, done)
+        return self._graphed(state, lstm_state, done, alias=alias)
 
     @torch.no_grad()
     def get_gae(self, next_obs, next_done, rewards, dones, values):
@@ -259,8 +260,22 @@ class GraphedPolicy:
         with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
             self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
 
-    def __call__(self, state, lstm_state, done):
-        if self.graph is None:
+    def _matches(self, state, lstm_state, done):
+        """The call has the captured shapes, dtypes and device (a broadcastable but different batch would
+        otherwise be silently broadcast by copy_ into the static buffers)."""
+        def same(a, b):
+            return a.shape == b.shape and a.dtype == b.dtype and a.device == b.device
+        if not (same(state, self.s_in) and same(done, self.s_done)):
+            return False
+        if self.s_lstm is None:
+            return lstm_state is None
+        return lstm_state is not None and same(lstm_state[0], self.s_lstm[0]) and same(lstm_state[1], self.s_lstm[1])
+
+    def __call__(self, state, lstm_state, done, alias=False):
+        """One replay.  ``alias=False`` (the default) returns copies, as ``get_action`` would; ``alias=True``
+        returns the graph's output buffers themselves, which the next replay overwrites (the rollout loop
+        copies them into its storage right away, train.py)."""
+        if self.graph is None or not self._matches(state, lstm_state, done):
             self._capture(state, lstm_state, done)
         self.s_in.copy_(state)
         self.s_done.copy_(done)
@@ -269,4 +284,7 @@ class GraphedPolicy:
             self.s_lstm[0].copy_(lstm_state[0])
             self.s_lstm[1].copy_(lstm_state[1])
         self.graph.replay()
-        return self.out
+        if alias:
+            return self.out
+        return tuple(None if x is None else (tuple(y.clone() for y in x) if isinstance(x, tuple) else x.clone())
+                     for x in self.out)

@@ -1,6 +1,6 @@
 """Recurrent PPO / RPO-LSTM training driver on the HIP env (RPO-LSTM/main.py:28-124, PPO/main.py).
 
-    python -m ouzelum_amd.learners.train --env EKFLeeLanded --num_envs 4096 --POMDP flicker --pomdp_prob 0.1
+    python -m ouzelum_amd.learners.train --env Landing --num_envs 4096 --POMDP flicker --pomdp_prob 0.1
 
 Same loop as the reference: T-step rollout with the LSTM carry reset on done, the
 actor acting on the clean observations and training on the learner-side POMDP ones
@@ -29,7 +29,7 @@ from .wrappers import ExtractObsWrapper, POMDPWrapper, RecordEpisodeStatisticsTo
 def parse_args(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--algo", default="rpo_lstm", choices=["rpo_lstm", "ppo"])
-    p.add_argument("--env", default="EKFLeeLanded")
+    p.add_argument("--env", default="Landing")              # RPO-LSTM/main.py:18 (every reference learner)
     p.add_argument("--seed", default=0, type=int)
     p.add_argument("--num_envs", type=int, default=4096)
     p.add_argument("--rollout_steps", type=int, default=16)
@@ -96,7 +96,7 @@ def train(args):
             obs[step] = next_obs
             dones[step] = next_done
             act_in = pomdp if args.rollout_obs == "pomdp" else next_obs
-            action, logprob, _, lstm_state = agent.act(act_in, lstm_state, next_done)
+            action, logprob, _, lstm_state = agent.act(act_in, lstm_state, next_done, alias=True)
             actions[step] = action
             logprobs[step] = logprob
             next_obs, rewards[step], next_done, info = envs.step(action)

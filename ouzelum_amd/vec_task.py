@@ -29,7 +29,8 @@ from . import _lib as L
 from .spaces import Box
 
 TASK_IDS = {"Ouzelum": L.TASK_OUZELUM, "LeeLanded": L.TASK_LEE_LANDED, "EKFLeeLanded": L.TASK_EKF_LEE_LANDED,
-            "QuadTracking": L.TASK_TRACKING, "QuadFault": L.TASK_FAULT, "QuadMixed": L.TASK_MIXED}
+            "QuadTracking": L.TASK_TRACKING, "QuadFault": L.TASK_FAULT, "QuadMixed": L.TASK_MIXED,
+            "Landing": L.TASK_LANDING}
 POMDP_IDS = {None: -1, "none": L.POMDP_NONE, "flicker": L.POMDP_FLICKER, "random_noise": L.POMDP_NOISE,
              "flickering_and_random_noise": L.POMDP_FLICKER_NOISE}
 

@@ -8,7 +8,9 @@ import numpy as np
 from oracle import quad_oracle as Q
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-GLUE = {"ekf": "EKFLeeLanded", "ekf_flicker": "EKFLeeLanded", "lee": "LeeLanded", "ouz": "Ouzelum"}
+GLUE = {"ekf": "EKFLeeLanded", "ekf_flicker": "EKFLeeLanded", "lee": "LeeLanded", "ouz": "Ouzelum",
+        "landing": "Landing"}
+PLAT_KEYS = ("plat", "plat_heading", "traj_type", "traj_idx", "traj_sd")
 
 
 def load(name):
@@ -20,7 +22,7 @@ def oracle_config(name, fx, n=None):
     task = GLUE[name]
     return Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n or fx["init_p"].shape[0], seed=int(fx["seed"]),
                        convergence_time=int(fx["convergence_time"]), pomdp_prob=float(fx["pomdp_prob"])
-                       if task != "Ouzelum" else None)
+                       if task not in ("Ouzelum", "Landing") else None)
 
 
 def state(fx, t, name):
@@ -28,16 +30,26 @@ def state(fx, t, name):
     n = fx["init_p"].shape[0]
     if t < 0:
         task_z = 1.0 if GLUE[name] == "Ouzelum" else 0.377
+        tgt = np.tile([0.0, 0.0, task_z], (n, 1))
+        if GLUE[name] == "Landing":
+            tgt[:, 0:2] = fx["init_plat"]
+            tgt[:, 0] += 0.08
         st = {"p": fx["init_p"], "q": fx["init_q"], "v": fx["init_v"], "w": fx["init_w"],
               "progress": fx["init_progress"], "reset": fx["init_reset"], "timeouts": np.zeros(n, bool),
               "thrust": np.zeros((n, 4)), "prev_v": np.zeros((n, 3)), "ekf_q": np.zeros((n, 4)),
               "ekf_P": np.broadcast_to(np.eye(4), (n, 4, 4)).copy(), "pv_x": np.zeros((n, 9)),
               "pv_P": np.broadcast_to(np.eye(9) * Q.PV_P0, (n, 9, 9)).copy(), "waypoint": np.zeros((n, 3)),
-              "target": np.tile([0.0, 0.0, task_z], (n, 1)), "sim_step": 0}
+              "target": tgt, "sim_step": 0}
+        for k in PLAT_KEYS:
+            if f"init_{k}" in fx:
+                st[k] = fx[f"init_{k}"]
         return st
     st = {k: fx[k][t] for k in ("p", "q", "v", "w", "progress", "reset", "timeouts", "thrust", "target")}
     for k in ("prev_v", "ekf_q", "ekf_P", "pv_x", "pv_P", "waypoint"):
         st[k] = fx[k][t] if k in fx else state(fx, -1, name)[k]
+    for k in PLAT_KEYS:
+        if k in fx:
+            st[k] = fx[k][t]
     st["sim_step"] = t + 1
     return st
 
@@ -56,6 +68,12 @@ def to_oracle(o, st):
     o.pv_P = np.array(st["pv_P"], np.float64)
     o.waypoint = np.array(st["waypoint"], np.float64)
     o.sim_step = int(st["sim_step"])
+    if "plat" in st:
+        o.plat = np.array(st["plat"], np.float64)
+        o.plat_heading = np.array(st["plat_heading"], np.float64)
+        o.traj_type = np.array(st["traj_type"], np.int64)
+        o.traj_idx = np.array(st["traj_idx"], np.int64)
+        o.traj_sd = np.array(st["traj_sd"], np.float64)
 
 
 def to_gpu(env, st):
@@ -74,6 +92,12 @@ def to_gpu(env, st):
     env.set_frows(L.F_PV_P, pack_sym(np.asarray(st["pv_P"]), 9).T)
     env.set_frows(L.F_WAYPOINT, np.asarray(st["waypoint"]).T)
     env.set_irows(L.I_PROGRESS, np.asarray(st["progress"]))
+    if "plat" in st:
+        env.set_frows(L.F_PLAT, np.asarray(st["plat"]).T)
+        env.set_frows(L.F_PLAT_HEADING, np.asarray(st["plat_heading"]))
+        env.set_frows(L.F_TRAJ_SD, np.asarray(st["traj_sd"]))
+        env.set_irows(L.I_TRAJ_TYPE, np.asarray(st["traj_type"]))
+        env.set_irows(L.I_TRAJ_IDX, np.asarray(st["traj_idx"]))
     env.reset_buf.copy_(torch.as_tensor(np.asarray(st["reset"]), dtype=torch.int64))
     env.timeout_buf.copy_(torch.as_tensor(np.asarray(st["timeouts"]), dtype=torch.bool))
     L.check(L.lib.ouz_set_step(env._env, int(st["sim_step"])), "ouz_set_step")

@@ -53,7 +53,8 @@ sys.path.insert(0, ROOT)
 from oracle import philox as rng  # noqa: E402
 from oracle import quad_oracle as Q  # noqa: E402
 
-TASK_IDS = {"EKFLeeLanded": Q.TASK_EKF_LEE_LANDED, "LeeLanded": Q.TASK_LEE_LANDED, "Ouzelum": Q.TASK_OUZELUM}
+TASK_IDS = {"EKFLeeLanded": Q.TASK_EKF_LEE_LANDED, "LeeLanded": Q.TASK_LEE_LANDED, "Ouzelum": Q.TASK_OUZELUM,
+            "Landing": Q.TASK_LANDING}
 
 
 # --------------------------------------------------------------------------------------------- stubs
@@ -85,6 +86,7 @@ class _Draws:
     ids = None           # env ids of the reset_idx / set_targets call in progress
     calls = 0
     in_targets = False   # inside set_targets: torch.rand draws goals, not POMDP coins
+    in_traj = False      # inside reset_completed_trajectories: new trajectory draws
     coins = []           # POMDPWrapper.observation coins of this step, in call order
     noise = []           # POMDPWrapper noise tensors, in call order
 
@@ -114,6 +116,10 @@ class _TorchProxy(types.ModuleType):
 
     @staticmethod
     def rand(*size, device=None, **kw):
+        if D.in_traj:                                     # trajectory scale (landing.py:228)
+            w = rng.draw_u32(D.seed, D.ids.numpy(), D.step, rng.RNG_TRAJ)
+            assert tuple(kw["size"]) == (len(D.ids),)
+            return torch.tensor(rng.u32_to_unit_f32(w[1]), dtype=torch.float32)
         if not D.in_targets:                              # POMDPWrapper.observation coin (POMDP.py:25,35)
             assert size == (1,), size
             return torch.tensor([D.coins.pop(0)], dtype=torch.float32)
@@ -125,6 +131,15 @@ class _TorchProxy(types.ModuleType):
         assert size == (len(ids),), size
         return torch.tensor(u[2])
 
+    @staticmethod
+    def randint(low, high, size, dtype=None, **kw):
+        """Trajectory type (high 3) and direction (high 2) of reset_completed_trajectories (landing.py:226-229):
+        words 0 and 2 of the env's RNG_TRAJ draw, as the kernel's new-trajectory draw uses them."""
+        assert D.in_traj and low == 0 and tuple(size) == (len(D.ids),)
+        w = rng.draw_u32(D.seed, D.ids.numpy(), D.step, rng.RNG_TRAJ)
+        v = (w[0] % np.uint32(3)) if high == 3 else (w[2] & np.uint32(1))
+        return torch.tensor(v.astype(np.int64), dtype=dtype)
+
     class FloatTensor:                                     # POMDP.py:30,37: FloatTensor(*shape).uniform_(lo, hi)
         def __init__(self, *shape):
             self.shape = shape
@@ -133,6 +148,18 @@ class _TorchProxy(types.ModuleType):
             t = D.noise.pop(0)
             assert tuple(t.shape) == tuple(self.shape)
             return t
+
+
+def get_euler_xyz(q):
+    """isaacgym.torch_utils.get_euler_xyz (closed package): the standard xyzw -> (roll, pitch, yaw) formula,
+    each wrapped to [0, 2 pi) as isaacgym does.  Landing reads the husky's yaw with it (landing.py:361)."""
+    x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    roll = torch.atan2(2.0 * (w * x + y * z), w * w - x * x - y * y + z * z)
+    sinp = 2.0 * (w * y - z * x)
+    pitch = torch.where(torch.abs(sinp) >= 1, torch.sign(sinp) * (math.pi / 2.0), torch.asin(sinp.clamp(-1, 1)))
+    yaw = torch.atan2(2.0 * (w * z + x * y), w * w + x * x - y * y - z * z)
+    two_pi = 2.0 * math.pi
+    return roll % two_pi, pitch % two_pi, yaw % two_pi
 
 
 def install_stubs(ref):
@@ -148,6 +175,7 @@ def install_stubs(ref):
     gymutil = _module("isaacgym.gymutil")
     gymutil.__getattr__ = lambda k: _Any(k)
     tu = _module("isaacgym.torch_utils", quat_rotate=rot.quat_rotate, torch_rand_float=torch_rand_float,
+                 get_euler_xyz=get_euler_xyz,
                  tensor_clamp=lambda t, lo, hi: torch.max(torch.min(t, hi), lo),
                  to_torch=lambda x, dtype=torch.float, device="cuda:0", requires_grad=False: torch.tensor(
                      x, dtype=dtype, requires_grad=requires_grad))
@@ -163,12 +191,13 @@ def install_stubs(ref):
         m.__path__ = [os.path.join(root, sub)]
     mods = {}
     for name in ("isaacgymenvs.tasks.base.vec_task", "isaacgymenvs.utils.POMDP", "isaacgymenvs.tasks.ekf_lee_landed",
-                 "isaacgymenvs.tasks.lee_landed", "isaacgymenvs.tasks.ouzelum"):
+                 "isaacgymenvs.tasks.lee_landed", "isaacgymenvs.tasks.ouzelum", "isaacgymenvs.tasks.landing"):
         mods[name.rsplit(".", 1)[1]] = importlib.import_module(name)
     proxy = _TorchProxy()
     mods["POMDP"].torch = proxy
     mods["ouzelum"].torch = proxy
-    for k in ("ekf_lee_landed", "lee_landed", "ouzelum"):
+    mods["landing"].torch = proxy
+    for k in ("ekf_lee_landed", "lee_landed", "ouzelum", "landing"):
         mods[k].torch_rand_float = torch_rand_float      # bound by the star import of torch_jit_utils
     return mods
 
@@ -201,6 +230,9 @@ class StubGym:
         self.env = env
         self.forces = self.torques = None
 
+    def set_dof_velocity_target_tensor(self, sim, dof_vel):
+        self.dof_targets = dof_vel.detach().clone()
+
     def apply_rigid_body_force_tensors(self, sim, forces, torques, space):
         assert space == 1                                 # gymapi.LOCAL_SPACE
         self.forces = forces.detach().clone()
@@ -217,11 +249,27 @@ class StubGym:
             f_b = f[:, 0, :].numpy()
             tau_b = self.torques[:, 0, :].double().numpy()
         e._last_wrench = (f_b.copy(), tau_b.copy())
+        n = f_b.shape[0]
+        plat, plat_v = np.zeros((n, 2)), np.zeros((n, 2))
+        if e._husky_drive:
+            # the husky as the build's kinematic differential-drive unicycle driven by the wheel
+            # speed targets set_husky_actions gave PhysX (right, left, right, left; landing.py:362-363)
+            wr = self.dof_targets[:, 4:8].double().numpy()
+            right, left = wr[:, 0], wr[:, 1]
+            lin = Q.WHEEL_RADIUS * (left + right) / 2.0
+            ang = Q.WHEEL_RADIUS * (left - right) / Q.WHEEL_BASE
+            _, _, yaw = get_euler_xyz(e.husky_quats)
+            th = Q.map_to_pi(Q.map_to_pi(yaw.double().numpy()) + ang * Q.DT)
+            plat_v = np.stack([lin * np.cos(th), lin * np.sin(th)], 1)
+            plat = e.husky_states[:, 0:2].double().numpy() + plat_v * Q.DT
+            e.husky_states[:, 0:2] = torch.from_numpy(plat)
+            e.husky_states[:, 3:7] = torch.from_numpy(np.stack([np.zeros(n), np.zeros(n), np.sin(th / 2),
+                                                                np.cos(th / 2)], 1))
+            e._heading = th
         rs = e.root_states
         p, q, v, w = (rs[:, 0:3].numpy().copy(), rs[:, 3:7].numpy().copy(), rs[:, 7:10].numpy().copy(),
                       rs[:, 10:13].numpy().copy())
-        n = p.shape[0]
-        deck = (np.full(n, not e._rotor_forces), np.zeros((n, 2)), np.zeros((n, 2)))
+        deck = (np.full(n, not e._rotor_forces or e._husky_drive), plat, plat_v)
         p, q, v, w = Q.integrate(p, q, v, w, f_b, tau_b, np.full(n, Q.MASS), np.broadcast_to(Q.INERTIA, (n, 3)),
                                  Q.DT, Q.SUBSTEPS, contact=deck)
         rs[:, 0:3] = torch.from_numpy(p)
@@ -236,7 +284,7 @@ class StubGym:
 def make_env(mods, task, n, pomdp_prob, conv):
     """An instance of the reference task class without __init__, holding what __init__ creates."""
     modname, clsname = {"EKFLeeLanded": ("ekf_lee_landed", "EKFLeeLanded"), "LeeLanded": ("lee_landed", "LeeLanded"),
-                        "Ouzelum": ("ouzelum", "Ouzelum")}[task]
+                        "Ouzelum": ("ouzelum", "Ouzelum"), "Landing": ("landing", "Landing")}[task]
     mod = mods[modname]
     Base = getattr(mod, clsname)
 
@@ -244,6 +292,15 @@ def make_env(mods, task, n, pomdp_prob, conv):
         def reset_idx(self, env_ids):
             D.ids, D.calls = env_ids.clone(), 0
             return Base.reset_idx(self, env_ids)
+
+        def reset_completed_trajectories(self, *a, **k):
+            done = (self.target_indices == self.num_waypoints) | ((self.husky_trajectories == 2) &
+                                                                  (self.target_indices > 3))
+            D.ids, D.in_traj = torch.nonzero(done).flatten(), True
+            try:
+                return Base.reset_completed_trajectories(self, *a, **k)
+            finally:
+                D.in_traj = False
 
         def set_targets(self, env_ids):
             D.ids, D.in_targets = env_ids.clone(), True
@@ -269,8 +326,9 @@ def make_env(mods, task, n, pomdp_prob, conv):
     e.gym = StubGym(e)
     e.sim_params = types.SimpleNamespace(dt=dt, gravity=types.SimpleNamespace(x=0.0, y=0.0, z=-9.81))
     e.dt = dt
-    e._rotor_forces = task == "Ouzelum"
-    e.max_episode_length = {"EKFLeeLanded": 700, "LeeLanded": 2000, "Ouzelum": 2000}[task]   # cfg/task/*.yaml
+    e._rotor_forces = task in ("Ouzelum", "Landing")
+    e._husky_drive = task == "Landing"
+    e.max_episode_length = {"EKFLeeLanded": 700, "LeeLanded": 2000, "Ouzelum": 2000, "Landing": 2000}[task]
     vec_root = torch.zeros((n, 2, 13))
     e.root_states = vec_root[:, 0, :]
     e.root_positions = e.root_states[:, 0:3]
@@ -279,6 +337,8 @@ def make_env(mods, task, n, pomdp_prob, conv):
     e.root_angvels = e.root_states[:, 10:13]
     e.husky_states = e.marker_states = vec_root[:, 1, :]
     e.husky_positions = e.marker_positions = e.husky_states[:, 0:3]
+    e.husky_quats = e.husky_states[:, 3:7]
+    e.husky_states[:, 6] = 1.0
     e.dof_states = torch.zeros((n, 8, 2))
     e.dof_positions, e.dof_velocities = e.dof_states[..., 0], e.dof_states[..., 1]
     init = torch.zeros((n, 13))
@@ -289,6 +349,18 @@ def make_env(mods, task, n, pomdp_prob, conv):
     e.initial_dof_states = e.dof_states.clone()
     e.target_root_positions = torch.zeros((n, 3))
     e.target_root_positions[:, 2] = 1.0 if task == "Ouzelum" else 0.377
+    if task == "Landing":                                  # landing.py:108-112, _create_envs trajectory state
+        e.cfg["env"]["envSpacing"] = 2.5                   # cfg/task/Landing.yaml
+        e.num_waypoints = 100
+        e.leminiscate_waypoints = mod.lemniscate(a=4, num_points=100)
+        e.circle_waypoints = mod.circle(r=2, num_points=100)
+        e.square_waypoints = mod.square(side_length=4, num_points=8)
+        w = rng.draw_u32(D.seed, np.arange(n), rng.INIT_STEP, rng.RNG_TRAJ)   # the build's creation draws
+        e.target_positions = torch.zeros((n, 2), dtype=torch.float32)
+        e.husky_trajectories = torch.tensor((w[0] % np.uint32(3)).astype(np.int64), dtype=torch.uint8)
+        e.trajectories_scaling = torch.tensor(rng.uniform_f32(w[1], 0.8, 1.2))
+        e.trajectories_direction = torch.tensor(np.where(w[2] & np.uint32(1), 1.0, -1.0).astype(np.float32))
+        e.target_indices = torch.zeros(n).long()
     e.thrusts = torch.zeros((n, 4))
     e.forces = torch.zeros((n, 6 if task == "Ouzelum" else 20, 3))
     e.torques = torch.zeros((n, 20, 3))
@@ -343,7 +415,7 @@ def step_coins(task, step, n, conv, prob=0.0):
     (ahrs_ekf.py:1309) here, where the tensor sits on the CPU (on the reference's cuda:0 that copy raises too)."""
     t = TASK_IDS[task]
     none = np.zeros(n, bool)
-    if task == "Ouzelum":
+    if task in ("Ouzelum", "Landing"):                                            # no POMDP in the env
         return [], none
     if task == "LeeLanded":
         return [coin(step, rng.SITE_OBS, t)], none                               # lee_landed.py:367
@@ -368,14 +440,14 @@ def initial_state(task, n, seed):
     q = np.concatenate([ax * np.sin(ang / 2)[:, None], np.cos(ang / 2)[:, None]], 1)
     v = rs.normal(0, 0.4, (n, 3))
     w = rs.normal(0, 0.4, (n, 3))
-    maxlen = {"EKFLeeLanded": 700, "LeeLanded": 2000, "Ouzelum": 2000}[task]
+    maxlen = {"EKFLeeLanded": 700, "LeeLanded": 2000, "Ouzelum": 2000, "Landing": 2000}[task]
     prog = rs.randint(1, maxlen - 30, n)
     prog[0:3] = maxlen - 1 - np.array([0, 3, 9])          # time-outs during the run
     reset = (rs.uniform(0, 1, n) < 0.2).astype(np.int64)
     reset[3] = 1
     p[9] = [6.5, 5.5, 1.2]                                 # beyond the distance-8 die radius
     reset[9] = 0
-    if task == "Ouzelum":
+    if task in ("Ouzelum", "Landing"):
         prog[4:7] = [500, 1000, 499]                       # random goals due (ouzelum.py:221-224)
         p[7] = [0.0, 0.0, 0.52]                            # near the z < 0.5 die line
     else:
@@ -386,7 +458,21 @@ def initial_state(task, n, seed):
         v[4:7] = rs.normal(0, 0.05, (3, 3))
         if task == "LeeLanded":
             p[8] = [0.05, 0.05, 1.0]                       # inside LeeLanded's 0.2 cut of (0, 0, 1)
-    return {"p": p, "q": q, "v": v, "w": w, "progress": prog, "reset": reset}
+    out = {"p": p, "q": q, "v": v, "w": w, "progress": prog, "reset": reset}
+    if task == "Landing":
+        # husky trajectory state: the creation draws of the build (INIT_STEP), each husky near its current
+        # waypoint, a quarter of them at their trajectory's last waypoint (a new trajectory is drawn at once:
+        # reset_completed_trajectories, landing.py:215-235)
+        w_ = rng.draw_u32(seed, np.arange(n), rng.INIT_STEP, rng.RNG_TRAJ)
+        ttype = (w_[0] % np.uint32(3)).astype(np.int64)
+        sd = rng.uniform_f32(w_[1], 0.8, 1.2) * np.where(w_[2] & np.uint32(1), 1.0, -1.0)
+        tabs = Q.waypoint_tables()
+        lens = np.array([len(tabs[k]) for k in ttype])
+        idx = np.where(np.arange(n) % 4 == 0, lens - 1, rs.randint(0, 1 << 30, n) % (lens - 1))
+        wp = np.stack([tabs[k][i] for k, i in zip(ttype, idx)]) * sd[:, None]
+        out.update({"plat": wp + rs.uniform(-0.15, 0.15, (n, 2)), "plat_heading": rs.uniform(-np.pi, np.pi, n),
+                    "traj_type": ttype, "traj_idx": idx, "traj_sd": sd.astype(np.float32).astype(np.float64)})
+    return out
 
 
 def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
@@ -399,10 +485,17 @@ def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
     e.root_states[:, 10:13] = torch.tensor(s0["w"])
     e.progress_buf[:] = torch.tensor(s0["progress"])
     e.reset_buf[:] = torch.tensor(s0["reset"])
+    if task == "Landing":
+        e.husky_states[:, 0:2] = torch.tensor(s0["plat"])
+        h = s0["plat_heading"]
+        e.husky_states[:, 3:7] = torch.tensor(np.stack([0 * h, 0 * h, np.sin(h / 2), np.cos(h / 2)], 1))
+        e.target_indices[:] = torch.tensor(s0["traj_idx"])
+        e.target_root_positions[:, 0:2] = torch.tensor(s0["plat"])   # post_physics_step of the step before
+        e.target_root_positions[:, 0] += 0.08
     acts = np.random.RandomState(seed + 1).uniform(-1.3, 1.3, (steps, n, 4))
     rec = {k: [] for k in ("p", "q", "v", "w", "obs", "rew", "reset", "timeouts", "progress", "target", "f_b",
                            "tau_b", "thrust", "prev_v", "ekf_q", "ekf_P", "pv_x", "pv_P", "waypoint", "flag",
-                           "ekf_input_corrupted")}
+                           "ekf_input_corrupted", "plat", "plat_heading", "traj_type", "traj_idx", "traj_sd")}
     for t in range(steps):
         D.step = t
         D.coins, fired = step_coins(task, t, n, conv, pomdp_prob)
@@ -424,6 +517,12 @@ def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
         rec["f_b"].append(e._last_wrench[0])
         rec["tau_b"].append(e._last_wrench[1])
         rec["thrust"].append(e.thrusts.numpy().copy())
+        if task == "Landing":
+            rec["plat"].append(e.husky_states[:, 0:2].numpy().copy())
+            rec["plat_heading"].append(e._heading.copy())
+            rec["traj_type"].append(e.husky_trajectories.numpy().astype(np.int64))
+            rec["traj_idx"].append(e.target_indices.numpy().copy())
+            rec["traj_sd"].append((e.trajectories_scaling * e.trajectories_direction).numpy().astype(np.float64))
         if task == "EKFLeeLanded":
             rec["prev_v"].append(e.prev_root_linvels.numpy().copy())
             rec["ekf_q"].append(np.array(e.Q_state, dtype=np.float64))
@@ -517,6 +616,7 @@ def main():
             res["ekf_flicker"] = run_task(mods, "EKFLeeLanded", 42, 24, seed=6, pomdp_prob=0.15, conv=6)
             res["lee"] = run_task(mods, "LeeLanded", 40, 30, seed=7, pomdp_prob=0.2)
             res["ouz"] = run_task(mods, "Ouzelum", 40, 30, seed=8)
+            res["landing"] = run_task(mods, "Landing", 48, 120, seed=9)
             msg = ekf_input_corruption_raises(mods)
             assert msg, "the reference no longer raises on a corrupted EKF input: revisit step_coins"
             res["ekf_flicker"]["ekf_input_corruption_error"] = np.array(msg)

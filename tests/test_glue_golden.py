@@ -38,7 +38,7 @@ def _close(name, got, want, atol, rtol=0.0, mask=None):
 # f64 oracle vs the f64 reference run: the only differences are the build's f32-rounded random offsets and
 # operation order
 TOL = {"p": 1e-6, "q": 1e-6, "v": 1e-6, "w": 1e-5, "obs": 1e-6, "rew": 1e-6, "target": 1e-6, "f_b": 2e-5,
-       "tau_b": 2e-5, "thrust": 1e-6, "ekf_q": 1e-6, "waypoint": 1e-6, "prev_v": 1e-6}
+       "tau_b": 2e-5, "thrust": 1e-6, "ekf_q": 1e-6, "waypoint": 1e-6, "prev_v": 1e-6, "plat": 1e-5, "traj_sd": 1e-6}
 
 
 def compare(name, o, fx, t, mask=None):
@@ -46,6 +46,15 @@ def compare(name, o, fx, t, mask=None):
            "f_b": o.last_f_b, "tau_b": o.last_tau_b, "thrust": o.thrust}
     if G.GLUE[name] == "EKFLeeLanded":
         got.update({"ekf_q": G.quat_canon_wxyz(o.ekf_q), "waypoint": o.waypoint, "prev_v": o.prev_v})
+    if G.GLUE[name] == "Landing":
+        got.update({"plat": o.plat, "traj_sd": o.traj_sd})
+        dh = np.angle(np.exp(1j * (o.plat_heading - fx["plat_heading"][t])))
+        # the husky's f32 waypoint targets (landing.py:209-213 keeps them in float32) through the 1000 rad/rad
+        # heading gain (landing.py:364): 1e-7 round-off becomes ~1e-6 rad of heading
+        _close(f"{name}@{t} plat_heading", dh, np.zeros_like(dh), 1e-4, 0, mask)
+        for k, v in (("traj_type", o.traj_type), ("traj_idx", o.traj_idx)):
+            np.testing.assert_array_equal(v[mask] if mask is not None else v,
+                                          fx[k][t][mask] if mask is not None else fx[k][t], err_msg=f"{name}@{t} {k}")
     for k, v in got.items():
         want = G.quat_canon_wxyz(fx[k][t]) if k == "ekf_q" else fx[k][t]
         _close(f"{name}@{t} {k}", v, want, TOL[k], 1e-7, mask)
@@ -62,7 +71,7 @@ def compare(name, o, fx, t, mask=None):
         np.testing.assert_array_equal(a, b, err_msg=f"{name}@{t} {k}")
 
 
-@pytest.mark.parametrize("name", ["ekf", "lee", "ouz"])
+@pytest.mark.parametrize("name", ["ekf", "lee", "ouz", "landing"])
 def test_glue_free_run(name):
     """The oracle started from the fixture's start state and stepped with its actions reproduces the reference's
     whole trajectory (resets, time-outs, the convergence window, landings, random goals)."""
@@ -74,7 +83,7 @@ def test_glue_free_run(name):
         compare(name, o, fx, t)
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
 def test_glue_single_step(name):
     """One oracle step from every recorded reference state (exclusions: see the module docstring)."""
     fx = G.load(name)

@@ -37,7 +37,7 @@ def _close(name, got, want, atol, rtol, mask):
 def make_env(ouz, name, fx):
     task = G.GLUE[name]
     kw = dict(seed=int(fx["seed"]), task=task, num_envs=fx["init_p"].shape[0], sim_device="cuda:0")
-    if task != "Ouzelum":
+    if task not in ("Ouzelum", "Landing"):
         kw.update(pomdp="flicker", pomdp_prob=float(fx["pomdp_prob"]))
     if task == "EKFLeeLanded":
         kw["convergence_time"] = int(fx["convergence_time"])
@@ -52,7 +52,7 @@ def near_threshold(fx, t, name):
     return (np.abs(d - 8.0) < 1e-4) | (np.abs(p[:, 2] - z_die) < 1e-4)
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
 def test_gpu_step_from_reference_states(ouz, name):
     from ouzelum_amd import _lib as L
     fx = G.load(name)
@@ -78,8 +78,16 @@ def test_gpu_step_from_reference_states(ouz, name):
         np.testing.assert_array_equal(env.reset_buf.cpu().numpy()[m], fx["reset"][k][m], err_msg=f"{name}@{k}")
         np.testing.assert_array_equal(env.timeout_buf.cpu().numpy()[m], fx["timeouts"][k][m])
         np.testing.assert_array_equal(env.progress_buf.cpu().numpy()[m], fx["progress"][k][m])
-        if G.GLUE[name] == "Ouzelum":
+        if G.GLUE[name] in ("Ouzelum", "Landing"):
             _close(f"{name}@{k} thrust", f[L.F_THRUST:L.F_THRUST + 4].T, fx["thrust"][k], 1e-3, 1e-6, m)
+        if G.GLUE[name] == "Landing":
+            iv = env.irows(0, L.I_COUNT).cpu().numpy()
+            _close(f"{name}@{k} plat", f[L.F_PLAT:L.F_PLAT + 2].T, fx["plat"][k], 1e-5, 1e-6, m)
+            dh = np.angle(np.exp(1j * (f[L.F_PLAT_HEADING] - fx["plat_heading"][k])))
+            assert np.abs(dh[m]).max() < 1e-4, f"{name}@{k} heading"
+            np.testing.assert_array_equal(iv[L.I_TRAJ_TYPE][m], fx["traj_type"][k][m])
+            np.testing.assert_array_equal(iv[L.I_TRAJ_IDX][m], fx["traj_idx"][k][m])
+            _close(f"{name}@{k} traj_sd", f[L.F_TRAJ_SD], fx["traj_sd"][k], 1e-6, 1e-6, m)
         if ekf:
             _close(f"{name}@{k} ekf_q", G.quat_canon_wxyz(f[L.F_EKF_Q:L.F_EKF_Q + 4].T),
                    G.quat_canon_wxyz(fx["ekf_q"][k]), 2e-5, 0, m)
@@ -89,7 +97,7 @@ def test_gpu_step_from_reference_states(ouz, name):
             assert m.sum() > n // 2
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
 def test_gpu_pre_physics_wrench(ouz, name):
     """ouz_pre_physics from every recorded state: the body wrench the reference applied in the next step, and
     (EKF task) the filter / waypoint state its pre_physics_step left."""
