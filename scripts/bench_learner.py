@@ -2,7 +2,7 @@
 
 Times the reference loop shape (T = 16 rollout steps of policy + env.step, then one
 PPO update of 4 epochs x 2 minibatches) and splits wall time into rollout and update.
-    python scripts/bench_learner.py --env EKFLeeLanded --num_envs 4096 --iters 20
+    python scripts/bench_learner.py --env Landing --num_envs 4096 --iters 20
 """
 import argparse
 import json
@@ -18,7 +18,7 @@ from ouzelum_amd.vec_task import make  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--algo", default="rpo_lstm", choices=["rpo_lstm", "ppo"])
-ap.add_argument("--env", default="EKFLeeLanded")
+ap.add_argument("--env", default="Landing")   # the reference learners' default env (RPO-LSTM/main.py:18)
 ap.add_argument("--num_envs", type=int, default=4096)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=3)

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 TAG=${TAG:-r02}
-timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread \
+timeout -k 10 ${PYTEST_TIMEOUT:-600} python -u -m pytest tests -m gpu --maxfail=${MAXFAIL:-1} -q --timeout 150 --timeout-method thread \
   -p no:cacheprovider ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 15 gpurun_out/pytest_$TAG.log
 [ $rc -eq 0 ] || exit $rc

