@@ -243,10 +243,15 @@ class Runner:
         dev = self.dev
         if fused:
             self.prepare(steps)
+        # torch creates an event's HIP object lazily at its first record(); the first hipEventCreate of the
+        # process costs ~85 us of host time, which inside a 20-step region (~55 us of GPU work) would be
+        # most of the measured time.  Record both once before the region; the region re-records them.
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e1.record()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record()
         self.rollouts(steps, fused)

@@ -9,7 +9,24 @@ env whose tensors live on the GPU.
 The HIP library is loaded on first use of the env API (so ``ouzelum_amd.build``
 can rebuild it without loading a stale copy).
 """
+import os as _os
+import sys as _sys
+
 __all__ = ["make", "QuadVecTask", "TASK_IDS", "POMDP_IDS", "task_info"]
+
+# hipGraph replay: the ROCm runtime's graph packet-capture path (DEBUG_CLR_GRAPH_PACKET_CAPTURE, on by
+# default) replays a captured graph with racy, run-to-run different results once it engages after the
+# first few launches (a torch-only PPO-update graph drifts from its eager twin and from itself from the
+# ~9th replay; with the knob off every replay is bitwise equal: DESIGN.md §9,
+# scripts/exp/graph_update_repro.py).  The learners replay hipGraphs (learners/ppo.py GraphedPolicy), so
+# the knob is turned off here, before the HIP runtime reads its environment -- unless the caller set it.
+# GRAPH_REPLAY_SAFE is False when the runtime had already started before this import with the knob on:
+# graph replay is then not used.
+_tc = _sys.modules.get("torch.cuda")
+_hip_started = bool(_tc is not None and _tc.is_initialized())
+_knob_preset = "DEBUG_CLR_GRAPH_PACKET_CAPTURE" in _os.environ
+_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+GRAPH_REPLAY_SAFE = _os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] == "0" and (_knob_preset or not _hip_started)
 
 
 def __getattr__(name):

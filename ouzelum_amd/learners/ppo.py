@@ -28,6 +28,18 @@ from .. import _lib as L
 from .models import Critic, LSTMActor, MLPActor
 
 
+def _graph_replay_safe():
+    """hipGraph replay gives correct results only with the runtime's packet-capture path off (set by
+    ``ouzelum_amd/__init__.py`` before the HIP runtime starts)."""
+    import warnings
+    from .. import GRAPH_REPLAY_SAFE
+    if not GRAPH_REPLAY_SAFE and not getattr(_graph_replay_safe, "warned", False):
+        warnings.warn("HIP runtime started with DEBUG_CLR_GRAPH_PACKET_CAPTURE on: the rollout policy runs eagerly "
+                      "(import ouzelum_amd before initialising the GPU, or set the variable to 0)")
+        _graph_replay_safe.warned = True
+    return GRAPH_REPLAY_SAFE
+
+
 def broadcast_params(module, src=0):
     """Same initial weights on every rank (one flattened broadcast)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -122,7 +134,8 @@ class PPOLearner:
         unless ``OUZ_GRAPH_POLICY=0``.  Returns fresh tensors; ``alias=True`` returns the graph's static
         output tensors instead, overwritten by the next call (the rollout loop copies them into its
         buffers at once and passes the LSTM carry straight back)."""
-        if self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "1") == "0":
+        if (self.device.type != "cuda" or os.environ.get("OUZ_GRAPH_POLICY", "1") == "0"
+                or not _graph_replay_safe()):
             return self.get_action(state, lstm_state, done)
         if getattr(self, "_graphed", None) is None:
             self._graphed = GraphedPolicy(self)

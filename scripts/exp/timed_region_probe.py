@@ -56,4 +56,6 @@ print(json.dumps({"steps": a.steps, "flags": a.flags if a.flags is not None else
                   "sync_host_us_median": round(float(np.median(r[:, 1])), 2),
                   "wall_us_median": round(float(np.median(r[:, 0] + r[:, 1])), 2),
                   "gpu_events_us_median": round(float(np.median(r[:, 2])), 2),
-                  "wall_us_min": round(float((r[:, 0] + r[:, 1]).min()), 2)}))
+                  "wall_us_min": round(float((r[:, 0] + r[:, 1]).min()), 2),
+                  "first_reps_wall_us": [round((x[0] + x[1]) * 1e6, 1) for x in rows[:5]],
+                  "first_reps_gpu_us": [round(x[2] * 1e6, 1) for x in rows[:5]]}))
