@@ -32,11 +32,13 @@ constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS stagin
 // At or below this many envs a launch has at most 4 waves per CU and the step is latency-bound;
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
 constexpr int kLatencyRegimeEnvs = 65536;
+// s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt / lgkmcnt left at their maxima (no wait)
+constexpr int kWaitVmcnt0 = (0x7 << 4) | (0xF << 8);
 
 // Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
 // single-step kernel, read back with ouz_probe_stamps.  Not part of the product library.
 #ifdef OUZ_PROBE_STAMPS
-constexpr int kStampSlots = 13, kStampWaves = 1024;
+constexpr int kStampSlots = 32, kStampWaves = 1024;   // 0-12 step phases, 13-29 rollout step starts, 30-31 mid-rollout step
 __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
 #define OUZ_STAMP(k, wait)                                                                       \
   do {                                                                                           \
@@ -56,6 +58,7 @@ __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
 #else
 #define OUZ_STAMP(k, wait) do {} while (0)
 #define OUZ_STAMP_RT(k) do {} while (0)
+constexpr int kStampSlots = 0;
 #endif
 
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
@@ -629,7 +632,11 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       pomdp_apply<3>(vm, tp, task, a, sc, gid, SITE_VEL, false);
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
+#ifdef OUZ_PROBE_UNIFORM_TRIGGER   // probe only (wrong results): every lane takes its wave's first lane's triggers
+    const uint64_t g = (uint64_t)sc.step * a.n_total + __builtin_amdgcn_readfirstlane(gid);
+#else
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
+#endif
     {
       // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
       // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
@@ -907,7 +914,15 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
     OUZ_STAMP(6, false);
   } else {
+    // Drain the state loads before the step loop.  vmcnt counts loads and stores in one in-order counter,
+    // and the compiler's waits for the first use of each loaded register sat inside the loop body, where
+    // from the second step on they waited for the previous step's output stores instead.  One wait here
+    // (the loads were issued together: the first step pays that round trip anyway) leaves the loop with
+    // waits only for its own loads.  Measured effect small: SQ_WAIT_ANY 477 -> 463 wave quad-cycles per
+    // LeeLanded step at 4096 envs (profiles/r02/sq_*); the per-step time is VALU/SALU issue.
+    __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     for (int k = 0; k < K; ++k) {
+      if (kStampSlots > 13 && k <= 16) OUZ_STAMP(13 + k, false);
       float ob[OUZ_NUM_OBS];
       float rew = 0.0f;
       bool rs = false, to = false;
@@ -915,6 +930,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
       const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
       if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
+      if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT>(ctx[k + 1].actions, S);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i);
       OutPtrs o = outs[0];
@@ -928,7 +944,9 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       } else {
         emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
       }
+      if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
     }
+    if (kStampSlots > 13 && K <= 16) OUZ_STAMP(13 + K, false);
     if (stats_mode && valid) {
       // RecordEpisodeStatisticsTorch over the rollout (PPO/utils.py:20-35) without a separate launch: this
       // lane's totals (accumulated before + finished in these K steps, same f32 adds as the atomics of

@@ -22,7 +22,7 @@ acts = (torch.rand((n, 4), device="cuda") * 2 - 1).contiguous()
 for _ in range(300):
     env.step(acts)
 torch.cuda.synchronize()
-SLOTS = 13
+SLOTS = 32
 waves = min((n + 63) // 64, 1024)
 rows = []
 for rep in range(40):

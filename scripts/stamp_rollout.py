@@ -1,0 +1,54 @@
+"""Per-step timeline of the fused rollout kernel from per-wave s_memtime stamps (probe build with
+-DOUZ_PROBE_STAMPS, loaded through OUZ_LIB).  Slots 13..29: start of rollout steps 0..16 (29 = after the
+last step); 30 / 31: mid-rollout step (k = 8) after env_core / after its stores were issued; 2 / 3 / 4: the
+last step's reset-done / controller-done / physics-done.
+
+    OUZ_LIB=ouzelum_amd/libouzelum_probe.so python scripts/stamp_rollout.py LeeLanded 4096
+"""
+import ctypes
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import bench as B  # noqa: E402
+from ouzelum_amd import _lib  # noqa: E402
+from ouzelum_amd.distributed import ReturnAllReduce  # noqa: E402
+
+task = sys.argv[1] if len(sys.argv) > 1 else "LeeLanded"
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+lib = _lib.lib
+lib.ouz_probe_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+lib.ouz_probe_stamps.restype = ctypes.c_int
+SLOTS = 32
+dev = torch.device("cuda", 0)
+run = B.Runner(task, n, dev, 1234, 0, 1, ReturnAllReduce(dev, batch=1))
+p = run.plan(B.RING)
+buf = torch.zeros(3, dtype=torch.float64, device=dev)
+for _ in range(20):
+    p(buf.data_ptr())
+torch.cuda.synchronize()
+waves = min((n + 63) // 64, 1024)
+rows = []
+for rep in range(30):
+    p(buf.data_ptr())
+    torch.cuda.synchronize()
+    h = np.zeros(1024 * SLOTS, dtype=np.uint64)
+    assert lib.ouz_probe_stamps(h.ctypes.data, h.size) > 0
+    rows.append(h.reshape(1024, SLOTS)[:waves].astype(np.int64))
+st = np.concatenate(rows, 0)
+steps = np.diff(st[:, 13:30], axis=1)
+print(f"{task} N={n} fused rollout: {len(st)} wave samples; shader cycles per step (median over waves)")
+print("  per step k:", " ".join(f"{int(x)}" for x in np.median(steps, 0)))
+print(f"  step median {np.median(steps):.0f}  p90 {np.percentile(steps, 90):.0f}  (steps 1..15: {np.median(steps[:, 1:]):.0f})")
+print(f"  k=8: env_core {np.median(st[:, 30] - st[:, 21]):.0f}, emit {np.median(st[:, 31] - st[:, 30]):.0f}, "
+      f"to next step {np.median(st[:, 22] - st[:, 31]):.0f}")
+last = st[:, 28]
+print(f"  last step: prelude+reset {np.median(st[:, 2] - last):.0f}, controller {np.median(st[:, 3] - st[:, 2]):.0f}, "
+      f"physics {np.median(st[:, 4] - st[:, 3]):.0f}, post+emit {np.median(st[:, 29] - st[:, 4]):.0f}")
+if st[:, 12].any():
+    print(f"  last step estimator: inputs->EKF {np.median(st[:, 10] - st[:, 2]):.0f}, EKF {np.median(st[:, 11] - st[:, 10]):.0f}, "
+          f"PV {np.median(st[:, 12] - st[:, 11]):.0f}, guidance+Lee {np.median(st[:, 3] - st[:, 12]):.0f}")
+print(f"  launch: entry -> first step {np.median(st[:, 13] - st[:, 0]):.0f}, rollout {np.median(st[:, 29] - st[:, 13]):.0f}, "
+      f"after last step -> stores landed {np.median(st[:, 7] - st[:, 29]):.0f}")
