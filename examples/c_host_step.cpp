@@ -46,8 +46,10 @@ int main(int argc, char** argv) {
   CHECK(ouz_create(&cfg, &env));
 
   ouz_buffers b{};
-  HIPCHECK(hipMalloc(&b.fstate, OUZ_TILED_SIZE(n, OUZ_F_COUNT) * sizeof(float)));
-  HIPCHECK(hipMalloc(&b.istate, OUZ_TILED_SIZE(n, OUZ_I_COUNT) * sizeof(int32_t)));
+  const int64_t slots = ouz_state_slots(cfg.task, n);   // == n except for the estimator tasks' class layout
+  if (slots < n) { std::fprintf(stderr, "ouz_state_slots: %s\n", ouz_last_error()); return 1; }
+  HIPCHECK(hipMalloc(&b.fstate, OUZ_TILED_SIZE(slots, OUZ_F_COUNT) * sizeof(float)));
+  HIPCHECK(hipMalloc(&b.istate, OUZ_TILED_SIZE(slots, OUZ_I_COUNT) * sizeof(int32_t)));
   HIPCHECK(hipMalloc(&b.obs, (size_t)n * OUZ_NUM_OBS * sizeof(float)));
   HIPCHECK(hipMalloc(&b.rew, (size_t)n * sizeof(float)));
   HIPCHECK(hipMalloc(&b.reset, (size_t)n * sizeof(int64_t)));

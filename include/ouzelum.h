@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define OUZ_ABI_VERSION 1
+#define OUZ_ABI_VERSION 2   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -91,8 +91,21 @@ extern "C" {
  *   fstate[ceil(num_envs/64)][OUZ_F_COUNT][64],  istate[...][OUZ_I_COUNT][64].
  * Field f of env i lives at OUZ_FIDX(f, i, OUZ_F_COUNT).  A wave's whole state
  * is one contiguous block, so its field loads walk DRAM pages in order instead
- * of touching OUZ_F_COUNT rows num_envs*4 bytes apart.  Buffers must hold
- * OUZ_TILED_SIZE(num_envs, count) elements; padding lanes are never touched. */
+ * of touching OUZ_F_COUNT rows num_envs*4 bytes apart.
+ *
+ * State slots.  The tiles hold ouz_state_slots(task, num_envs) slots.  For most
+ * tasks that is num_envs and slot i is env i.  The estimator tasks
+ * (OUZ_TASK_EKF_LEE_LANDED, OUZ_TASK_TRACKING) up to 65536 envs (the latency
+ * regime; above it the step is HBM-bound and slot i is env i) use the
+ * trigger-class layout: the
+ * PV filter's shared trigger counters (ekf_lee_landed.py:425-440) fire on
+ * g % 7 == 6 and g % 3 == 0 of g = step * num_envs_total + global id, so slots
+ * are grouped in blocks of 21 tiles (1344 slots) and tile k of block b holds
+ * envs b*1344 + k + 21*lane: one trigger class per wave.  The slot count is
+ * rounded up to a multiple of 1344; padding slots stay zero.  Slot of env e:
+ * b*1344 + (r % 21)*64 + r/21 with b = e/1344, r = e - b*1344.  Buffers must
+ * hold OUZ_TILED_SIZE(ouz_state_slots(task, num_envs), count) elements.  The
+ * env-order buffers (obs, rew, reset, time_outs, actions) are indexed by env. */
 #define OUZ_TILE 64
 #define OUZ_TILES(n) (((n) + OUZ_TILE - 1) / OUZ_TILE)
 #define OUZ_TILED_SIZE(n, count) ((size_t)OUZ_TILES(n) * (count) * OUZ_TILE)
@@ -198,6 +211,8 @@ typedef struct ouz_task_info {
 typedef struct ouz_env ouz_env;
 
 int32_t ouz_abi_version(void);
+/* State slots of a task at num_envs (see "State slots" above); negative on bad arguments. */
+int64_t ouz_state_slots(int32_t task, int32_t num_envs);
 const char* ouz_last_error(void);
 void ouz_default_config(ouz_config* cfg);
 int ouz_task_info_get(int32_t task, ouz_task_info* out);

@@ -22,7 +22,7 @@ class OuzelumError(RuntimeError):
 
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
-ABI_VERSION = 1
+ABI_VERSION = 2
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
@@ -83,6 +83,7 @@ _I64 = ctypes.c_int64
 # name -> (restype, argtypes).  This table IS the list of symbols include/ouzelum.h declares.
 SIGNATURES = {
     "ouz_abi_version": (_I, []),
+    "ouz_state_slots": (_I64, [_I, _I]),
     "ouz_last_error": (ctypes.c_char_p, []),
     "ouz_default_config": (None, [ctypes.POINTER(OuzConfig)]),
     "ouz_task_info_get": (_I, [_I, ctypes.POINTER(OuzTaskInfo)]),

@@ -35,6 +35,36 @@ constexpr int kLatencyRegimeEnvs = 65536;
 // s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt / lgkmcnt left at their maxima (no wait)
 constexpr int kWaitVmcnt0 = (0x7 << 4) | (0xF << 8);
 
+// Trigger-class slot layout of the estimator tasks.  The PV filter's shared trigger
+// counters fire the position fix on g % 7 == 6 and the velocity fix on g % 3 == 0 (g = step * N_total +
+// global id, ekf_lee_landed.py:425-440), so an env's trigger pattern is fixed by its id mod 21.  The state
+// slots of these tasks are grouped in blocks of 21 waves (1344 slots): wave k of block b holds envs
+// b*1344 + k + 21*l (l = lane), one trigger class per wave, so the PV corrections are wave-uniform
+// branches instead of every wave paying for both.  Slots past num_envs are idle lanes; the env-order
+// buffers (obs, rew, reset, time_outs, actions) are indexed by env.
+constexpr int kTrigClasses = 21;
+constexpr int kClassBlock = kTrigClasses * 64;
+// Latency regime only: at large N the env-order buffers' per-lane accesses 21 envs apart would cost more
+// HBM traffic (a 64-byte line per lane for the 8-byte reset flag, measured 0.74 -> 0.30 of HBM peak at
+// 4 M envs) than the uniform triggers save; there the step is HBM-bound and keeps slot i = env i.
+__host__ __device__ constexpr bool class_layout_task(int task) {
+  return task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING;
+}
+__host__ __device__ constexpr bool class_layout(int task, int n) {
+  return class_layout_task(task) && n <= kLatencyRegimeEnvs;
+}
+__host__ __device__ inline int state_slots(int task, int n) {
+  return class_layout(task, n) ? ((n + kClassBlock - 1) / kClassBlock) * kClassBlock : n;
+}
+__host__ __device__ inline int slot_env(int s) {   // class layout: env held by state slot s
+  const int b = s / kClassBlock, r = s - b * kClassBlock;
+  return b * kClassBlock + (r >> 6) + kTrigClasses * (r & 63);
+}
+__host__ __device__ inline int env_slot(int e) {   // its inverse
+  const int b = e / kClassBlock, r = e - b * kClassBlock;
+  return b * kClassBlock + (r % kTrigClasses) * 64 + r / kTrigClasses;
+}
+
 // Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
 // single-step kernel, read back with ouz_probe_stamps.  Not part of the product library.
 #ifdef OUZ_PROBE_STAMPS
@@ -112,6 +142,8 @@ struct StepArgs {
   uint8_t* timeouts;
   const float2* wp_tab;        // lemniscate[100] | circle[100] | square[4]
   int32_t n;
+  int32_t n_slots;             // state slots: n, or the trigger-class layout's padded count
+  int32_t cls;                 // 1: trigger-class slot layout (estimator tasks)
   uint32_t env_offset;
   uint64_t n_total;
   uint64_t seed;
@@ -338,14 +370,15 @@ __device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL,
   if constexpr (CTRL == CTRL_RL) S.act = reinterpret_cast<const float4*>(actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
 }
 
-template <int CTRL, int TGT>
+template <int CTRL, int TGT, bool CLS = false>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S,
                                          const float* actions) {
   // reset_buf and time_outs are read unconditionally and combined without a branch, so the two flag
   // loads and the state loads below are in flight together (one memory round trip, not three:
   // a short-circuit `!rst && timeouts == 0` made the time-out load wait for the reset load).
-  const int64_t rv = (a.reset + S.T.first)[S.T.l];
-  const uint32_t tv = (a.timeouts + S.T.first)[S.T.l];
+  // i: env index (the class layout's env-order buffers are not lane-contiguous)
+  const int64_t rv = CLS ? a.reset[i] : (a.reset + S.T.first)[S.T.l];
+  const uint32_t tv = CLS ? a.timeouts[i] : (a.timeouts + S.T.first)[S.T.l];
   S.rst = rv != 0;
   S.flags_clear = (rv == 0) & (tv == 0u);
   S.p = ld3(S.T, OUZ_F_P);
@@ -785,6 +818,24 @@ struct OutPtrs {
   uint8_t* timeouts;
 };
 
+// One lane's outputs by env index e (the trigger-class layout: a wave's envs are 21 apart): the 52-byte obs
+// row as three 16-byte stores + one dword, reward / flags at [e].
+__device__ __forceinline__ void emit_env(const OutPtrs& o, int e, bool valid, const float* ob, float rew, bool rs,
+                                         bool to, bool keep_flags) {
+  if (!valid) return;
+  typedef float f4a4 __attribute__((ext_vector_type(4), aligned(4)));
+  float* row = o.obs + (size_t)e * OUZ_NUM_OBS;
+  OUZ_ST(reinterpret_cast<f4a4*>(row), (f4a4{ob[0], ob[1], ob[2], ob[3]}));
+  OUZ_ST(reinterpret_cast<f4a4*>(row + 4), (f4a4{ob[4], ob[5], ob[6], ob[7]}));
+  OUZ_ST(reinterpret_cast<f4a4*>(row + 8), (f4a4{ob[8], ob[9], ob[10], ob[11]}));
+  OUZ_ST(&row[12], ob[12]);
+  OUZ_ST(&o.rew[e], rew);
+  if (!(keep_flags && !rs)) {
+    OUZ_ST(&o.reset[e], (int64_t)(rs ? 1 : 0));
+    OUZ_ST(&o.timeouts[e], (uint8_t)(to ? 1 : 0));
+  }
+}
+
 __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, int n, bool valid, const float* ob,
                                      float rew, bool rs, bool to, bool direct, bool keep_flags = false) {
   const uint32_t lane = (uint32_t)i & 63u;
@@ -854,11 +905,11 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
 // Per-step reset count for the trace (metrics/<pomdp>_<prob>_ep_count.txt, ekf_lee_landed.py:315-320):
 // one atomic per wave with resets; env 0 clears the slot 32 steps ahead (fused rollouts run waves
 // at most 31 steps apart, and the capacity is >= 64).
-__device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bool did_reset, int i) {
+__device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bool did_reset, int slot, int e) {
   if (a.trace_cap <= 0) return;
   const uint64_t m = __ballot(did_reset);
-  if ((i & 63) == 0 && m) atomicAdd(&a.trace_resets[step % (uint32_t)a.trace_cap], (uint32_t)__popcll(m));
-  if (i == 0) a.trace_resets[(step + 32u) % (uint32_t)a.trace_cap] = 0u;
+  if ((slot & 63) == 0 && m) atomicAdd(&a.trace_resets[step % (uint32_t)a.trace_cap], (uint32_t)__popcll(m));
+  if (e == 0) a.trace_resets[(step + 32u) % (uint32_t)a.trace_cap] = 0u;
 }
 
 // K steps of one env: load once, K x (step + emit), store once.  MULTI = false is the single
@@ -868,18 +919,20 @@ struct LaneStats {
   double sum, cnt, len;
 };
 
-template <int CTRL, int TGT, bool MULTI, bool PRE = false>
+// i: state slot (its wave tile is wave-uniform); e: env index (== i except under the trigger-class layout,
+// CLS), which keys the RNG and indexes the env-order buffers.
+template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
-                                        size_t out_stride, float* wave_lds, int i, bool valid, int task,
+                                        size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
                                         bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
                                         float* wrench = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
-  const uint32_t gid = a.env_offset + (uint32_t)i;
+  const uint32_t gid = a.env_offset + (uint32_t)e;
   EnvRegs<CTRL, TGT> S;
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT>(a, i, tp, S, ctx[0].actions);
+  if (valid) env_load<CTRL, TGT, CLS>(a, e, tp, S, ctx[0].actions);
   // fused statistics: the episode accumulators of earlier (unfused) steps, in flight with the state
   float ep_sum_old = 0.0f;
   int32_t ep_cnt_old = 0, ep_len_old = 0;
@@ -896,8 +949,8 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     float rew = 0.0f;
     bool rs = false, to = false;
     const bool did_reset = valid && S.rst;
-    if (valid) env_core<CTRL, TGT, true>(a, ctx[0], i, gid, task, S, ob, rew, rs, to, wrench);
-    if (did_reset) a.reset[i] = 0;
+    if (valid) env_core<CTRL, TGT, true>(a, ctx[0], e, gid, task, S, ob, rew, rs, to, wrench);
+    if (did_reset) a.reset[e] = 0;
   } else if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
@@ -907,11 +960,12 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
 #else
     const bool did_reset = valid && S.rst;
     const bool flags_clear = valid && S.flags_clear;
-    if (valid) env_core<CTRL, TGT>(a, ctx[0], i, gid, task, S, ob, rew, rs, to);
-    trace_count(a, ctx[0].step, did_reset, i);
+    if (valid) env_core<CTRL, TGT>(a, ctx[0], e, gid, task, S, ob, rew, rs, to);
+    trace_count(a, ctx[0].step, did_reset, i, e);
 #endif
     OUZ_STAMP(5, false);
-    emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
+    if (CLS) emit_env(outs[1], e, valid, ob, rew, rs, to, flags_clear);
+    else emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
     OUZ_STAMP(6, false);
   } else {
     // Drain the state loads before the step loop.  vmcnt counts loads and stores in one in-order counter,
@@ -929,18 +983,25 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       const bool did_reset = valid && S.rst;
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
       const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
-      if (valid) env_core<CTRL, TGT>(a, ctx[k], i, gid, task, S, ob, rew, rs, to);
+      if (valid) env_core<CTRL, TGT>(a, ctx[k], e, gid, task, S, ob, rew, rs, to);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT>(ctx[k + 1].actions, S);   // next step's row, before emit
-      trace_count(a, ctx[k].step, did_reset, i);
+      trace_count(a, ctx[k].step, did_reset, i, e);
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
         o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
         o.rew += (size_t)k * out_stride;
         o.reset += (size_t)k * out_stride;
         o.timeouts += (size_t)k * out_stride;
-        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
-        if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+        if (CLS) {
+          emit_env(o, e, valid, ob, rew, rs, to, false);
+          if (k == K - 1) emit_env(outs[1], e, valid, ob, rew, rs, to, false);
+        } else {
+          emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+          if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+        }
+      } else if (CLS) {
+        emit_env(o, e, valid, ob, rew, rs, to, flags_clear);
       } else {
         emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
       }
@@ -1057,28 +1118,29 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, int n, int 
   }
 }
 
-template <int TASK, bool MULTI, bool PRE = false>
+template <int TASK, bool MULTI, bool PRE = false, bool CLS = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
   __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
-  const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;
+  const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
   const int first = i - (int)(threadIdx.x & 63);
-  if (first >= a.n) return;                 // whole wave past the end
-  const bool valid = i < a.n;
+  if (first >= (CLS ? a.n_slots : a.n)) return;   // whole wave past the end
+  const int e = CLS ? slot_env(i) : i;             // env index
+  const bool valid = e < a.n;
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
   if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-    run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE, CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LANDING) {
-    run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -1088,51 +1150,54 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     const bool vl = valid && t == OUZ_TASK_LEE_LANDED, vt = valid && t == OUZ_TASK_TRACKING;
     const bool vr = valid && !vl && !vt;
     if (__any(vl))
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vl,
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vl,
                                                   OUZ_TASK_LEE_LANDED, direct, sm, &ls, wrench);
     if (__any(vt))
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vt,
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vt,
                                              OUZ_TASK_TRACKING, direct, sm, &ls, wrench);
     if (__any(vr))
-      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, vr, OUZ_TASK_FAULT,
+      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
                                         direct, sm, &ls, wrench);
   }
-  if (sm) reduce_stats(*rst, a.n, first, ls);
+  if (sm) reduce_stats(*rst, CLS ? a.n_slots : a.n, first, ls);
 }
 
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
 // (~390 B): the host copies the argument block on every launch (≈0.6 us more host time per launch
 // for a 1.1 KB block, scripts/exp/launch_cost.hip), and at 4096 envs that host time is the bound.
-template <int TASK>
+template <int TASK, bool CLS = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false>(a, &c, 1, env_out, 0);
+  step_body<TASK, false, false, CLS>(a, &c, 1, env_out, 0);
 }
 
 // ouz_pre_physics: pre_physics_step alone, the body wrench to `wrench` [n][6].
-template <int TASK>
+template <int TASK, bool CLS = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx c, float* wrench) {
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false, true>(a, &c, 1, env_out, 0, nullptr, wrench);
+  step_body<TASK, false, true, CLS>(a, &c, 1, env_out, 0, nullptr, wrench);
 }
 
 // ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.
-template <int TASK>
+template <int TASK, bool CLS = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+  step_body<TASK, true, false, CLS>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
 __global__ void init_state_kernel(StepArgs a, int task_cfg) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const uint32_t gid = a.env_offset + (uint32_t)i;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;   // state slot
+  if (s >= a.n_slots) return;
+  for (int k = 0; k < OUZ_F_COUNT; ++k) st(a, k, s, 0.0f);
+  for (int k = 0; k < OUZ_I_COUNT; ++k) sti(a, k, s, 0);
+  const int e = a.cls ? slot_env(s) : s;                 // env index (padding slots stay zero)
+  if (e >= a.n) return;
+  const uint32_t gid = a.env_offset + (uint32_t)e;
   const int task = task_cfg == OUZ_TASK_MIXED ? mixed_task(gid) : task_cfg;
   const TaskParams& tp = a.tp[tp_slot(task)];
-  for (int k = 0; k < OUZ_F_COUNT; ++k) st(a, k, i, 0.0f);
-  for (int k = 0; k < OUZ_I_COUNT; ++k) sti(a, k, i, 0);
+  const int i = s;
   st(a, OUZ_F_P + 2, i, 1.0f);           // default_pose.p.z = 1 (ekf_lee_landed.py:228-229)
   st(a, OUZ_F_Q + 3, i, 1.0f);
   st(a, OUZ_F_TARGET + 2, i, tp.target_mode == TGT_GOAL ? 1.0f : 0.377f);   // ouzelum.py:73, ekf_lee_landed.py:87
@@ -1146,10 +1211,10 @@ __global__ void init_state_kernel(StepArgs a, int task_cfg) {
     sti(a, OUZ_I_TRAJ_TYPE, i, (int)(r.x % 3u));
     st(a, OUZ_F_TRAJ_SD, i, (r.z & 1u) ? uniform_f32(r.y, 0.8f, 1.2f) : -uniform_f32(r.y, 0.8f, 1.2f));
   }
-  for (int k = 0; k < OUZ_NUM_OBS; ++k) a.obs[(size_t)i * OUZ_NUM_OBS + k] = 0.0f;
-  a.rew[i] = 0.0f;
-  a.reset[i] = 1;                        // reset_buf starts at ones (vec_task.py:269-270)
-  a.timeouts[i] = 0;
+  for (int k = 0; k < OUZ_NUM_OBS; ++k) a.obs[(size_t)e * OUZ_NUM_OBS + k] = 0.0f;
+  a.rew[e] = 0.0f;
+  a.reset[e] = 1;                        // reset_buf starts at ones (vec_task.py:269-270)
+  a.timeouts[e] = 0;
 }
 
 __global__ void mark_reset_kernel(int64_t* reset, const int32_t* ids, int32_t n, int32_t n_envs) {
@@ -1177,7 +1242,7 @@ __global__ void __launch_bounds__(kStatsBlock) episode_stats_kernel(StepArgs a, 
   __shared__ double s_part[3][kStatsBlock / 64];
   __shared__ bool s_last;
   double acc[3] = {0.0, 0.0, 0.0};   // sum of returns, count, sum of lengths
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n_slots; i += gridDim.x * blockDim.x) {
     acc[0] += (double)ld(a, OUZ_F_EP_SUM, i);
     acc[1] += (double)ldi(a, OUZ_I_EP_CNT, i);
     acc[2] += (double)ldi(a, OUZ_I_EP_LEN, i);
@@ -1229,13 +1294,13 @@ __global__ void __launch_bounds__(kStatsOneBlock) episode_stats_one_block_kernel
   __shared__ double s_part[3][kStatsOneBlock / 64];
   double acc[3] = {0.0, 0.0, 0.0};   // sum of returns, count, sum of lengths
   constexpr int kUnroll = 4;
-  for (int base = threadIdx.x; base < a.n; base += kStatsOneBlock * kUnroll) {
+  for (int base = threadIdx.x; base < a.n_slots; base += kStatsOneBlock * kUnroll) {
     float s[kUnroll];
     int32_t c[kUnroll], l[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       const int i = base + u * kStatsOneBlock;
-      const bool ok = i < a.n;
+      const bool ok = i < a.n_slots;
       s[u] = ok ? ld(a, OUZ_F_EP_SUM, i) : 0.0f;
       c[u] = ok ? ldi(a, OUZ_I_EP_CNT, i) : 0;
       l[u] = ok ? ldi(a, OUZ_I_EP_LEN, i) : 0;
@@ -1246,7 +1311,7 @@ __global__ void __launch_bounds__(kStatsOneBlock) episode_stats_one_block_kernel
       acc[0] += (double)s[u];
       acc[1] += (double)c[u];
       acc[2] += (double)l[u];
-      if (drain && i < a.n) {
+      if (drain && i < a.n_slots) {
         st(a, OUZ_F_EP_SUM, i, 0.0f);
         sti(a, OUZ_I_EP_CNT, i, 0);
         sti(a, OUZ_I_EP_LEN, i, 0);
@@ -1448,6 +1513,11 @@ int ouz_probe_stamps(uint64_t* host, int32_t count) {
 #endif
 
 int32_t ouz_abi_version(void) { return OUZ_ABI_VERSION; }
+
+int64_t ouz_state_slots(int32_t task, int32_t num_envs) {
+  if (task < 0 || task >= OUZ_NUM_TASKS || num_envs <= 0) return fail(OUZ_ERR_INVALID, "ouz_state_slots: bad task / size");
+  return state_slots(task, num_envs);
+}
 const char* ouz_last_error(void) { return g_err.c_str(); }
 
 void ouz_default_config(ouz_config* c) {
@@ -1526,7 +1596,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
   r = hip_check(hipMalloc(&e->drn_dev, 2 * sizeof(ouz_dr_noise)), "hipMalloc(dr noise)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
-  const size_t n_tiles = (size_t)OUZ_TILES(cfg->num_envs);
+  const size_t n_tiles = (size_t)OUZ_TILES(state_slots(cfg->task, cfg->num_envs));
   r = hip_check(hipMalloc(&e->wave_partials, n_tiles * 3 * sizeof(double) + 64), "hipMalloc(wave partials)");
   if (r) { (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   e->wave_ticket = reinterpret_cast<uint32_t*>(e->wave_partials + n_tiles * 3);
@@ -1540,6 +1610,8 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   std::memset(&a, 0, sizeof(a));
   a.wp_tab = e->wp_tab;
   a.n = cfg->num_envs;
+  a.n_slots = state_slots(cfg->task, cfg->num_envs);
+  a.cls = class_layout(cfg->task, cfg->num_envs) ? 1 : 0;
   a.env_offset = (uint32_t)cfg->env_id_offset;
   a.n_total = (uint64_t)total;
   a.seed = cfg->seed;
@@ -1607,8 +1679,8 @@ int ouz_bind(ouz_env* env, const ouz_buffers* b) {
 int ouz_init_state(ouz_env* env, void* stream) {
   if (!env || !env->bound) return fail(OUZ_ERR_UNBOUND, "ouz_init_state: env not bound");
   const int n = env->cfg.num_envs, blk = block_for(n);
-  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(n, blk)), dim3(blk), 0, (hipStream_t)stream, env->args,
-                     env->cfg.task);
+  hipLaunchKernelGGL(init_state_kernel, dim3(grid_for(env->args.n_slots, blk)), dim3(blk), 0, (hipStream_t)stream,
+                     env->args, env->cfg.task);
   OUZ_LAUNCH_CHECK("init_state_kernel");
   env->step = 0;
   return OUZ_OK;
@@ -1633,6 +1705,20 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
   return m;
 }
 
+// One task's step or rollout kernel; the estimator tasks have a trigger-class-layout instantiation.
+extern "C++" template <int T>
+static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, dim3 g, dim3 b, hipStream_t s) {
+  if constexpr (class_layout_task(T)) {
+    if (a.cls) {
+      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g, b, 0, s, a, r.ctx[0]);
+      else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g, b, 0, s, a, r);
+      return;
+    }
+  }
+  if (single) hipLaunchKernelGGL((quad_step_kernel<T, false>), g, b, 0, s, a, r.ctx[0]);
+  else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
+}
+
 // Launch K (<= kMaxRolloutChunk) consecutive steps as ONE kernel.  K = 1 is VecTask.step.
 // ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
 // storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
@@ -1654,15 +1740,9 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
     r.ctx[k].flick_mask = flicker_mask(a, env->cfg.task, step);
     r.ctx[k].actions = ring ? ring + (size_t)((ring_pos + k) % ring_len) * n * OUZ_NUM_ACT : nullptr;
   }
-  dim3 g(grid_for(n, blk)), b(blk);
-#define OUZ_LAUNCH_TASK(T)                                         \
-  do {                                                             \
-    if (K == 1 && !storage && !stats_mode) {                       \
-      hipLaunchKernelGGL(quad_step_kernel<T>, g, b, 0, s, a, r.ctx[0]); \
-    } else {                                                       \
-      hipLaunchKernelGGL(quad_rollout_kernel<T>, g, b, 0, s, a, r); \
-    }                                                              \
-  } while (0)
+  dim3 g(grid_for(a.n_slots, blk)), b(blk);   // one lane per state slot
+  const bool single = K == 1 && !storage && !stats_mode;
+#define OUZ_LAUNCH_TASK(T) launch_task<T>(single, a, r, g, b, s)
   switch (env->cfg.task) {
     case OUZ_TASK_OUZELUM: OUZ_LAUNCH_TASK(OUZ_TASK_OUZELUM); break;
     case OUZ_TASK_LEE_LANDED: OUZ_LAUNCH_TASK(OUZ_TASK_LEE_LANDED); break;
@@ -1751,14 +1831,19 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
   const StepArgs& a = env->args;
   const int n = env->cfg.num_envs, blk = block_for(n);
   StepCtx c{(uint32_t)env->step, flicker_mask(a, env->cfg.task, (uint32_t)env->step), actions};
-  dim3 g(grid_for(n, blk)), b(blk);
+  dim3 g(grid_for(a.n_slots, blk)), b(blk);
   hipStream_t s = (hipStream_t)stream;
   switch (env->cfg.task) {
     case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_EKF_LEE_LANDED:
-      hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
-    case OUZ_TASK_TRACKING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_TRACKING>, g, b, 0, s, a, c, wrench); break;
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true>), g, b, 0, s, a, c, wrench);
+      else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, false>), g, b, 0, s, a, c, wrench);
+      break;
+    case OUZ_TASK_TRACKING:
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true>), g, b, 0, s, a, c, wrench);
+      else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, false>), g, b, 0, s, a, c, wrench);
+      break;
     case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LANDING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LANDING>, g, b, 0, s, a, c, wrench); break;
     default: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a, c, wrench); break;

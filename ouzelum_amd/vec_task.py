@@ -41,6 +41,14 @@ def task_info(task: int) -> L.OuzTaskInfo:
     return info
 
 
+def _class_layout_slots(n, device):
+    """State slot of each env under the trigger-class layout (include/ouzelum.h "State slots"; estimator tasks
+    up to 65536 envs): blocks of 1344 slots, tile k of block b holds envs b*1344 + k + 21*lane."""
+    e = torch.arange(n, device=device, dtype=torch.int64)
+    b, r = e // 1344, e % 1344
+    return b * 1344 + (r % 21) * 64 + r // 21
+
+
 class QuadVecTask:
     """Vectorised x500 quadrotor env (one HIP kernel per step)."""
 
@@ -103,9 +111,15 @@ class QuadVecTask:
 
         # --- buffers (owned here; allocate_buffers vec_task.py:254-277) ---
         with torch.cuda.device(self.device):
-            # wave-tiled SoA [tiles][fields][64] (include/ouzelum.h OUZ_FIDX); padding lanes stay 0
-            self.fstate = torch.zeros((L.tiles(n), L.F_COUNT, L.TILE), dtype=torch.float32, device=self.device)
-            self.istate = torch.zeros((L.tiles(n), L.I_COUNT, L.TILE), dtype=torch.int32, device=self.device)
+            # wave-tiled SoA [tiles][fields][64] over the task's state slots (include/ouzelum.h "State slots":
+            # the estimator tasks group envs by PV trigger class); padding slots stay 0
+            slots = int(L.lib.ouz_state_slots(self.task, n))
+            if slots < n:
+                raise L.OuzelumError(f"ouz_state_slots: {L.lib.ouz_last_error().decode()}")
+            self.fstate = torch.zeros((L.tiles(slots), L.F_COUNT, L.TILE), dtype=torch.float32, device=self.device)
+            self.istate = torch.zeros((L.tiles(slots), L.I_COUNT, L.TILE), dtype=torch.int32, device=self.device)
+            # env -> state slot (None: slot i is env i)
+            self._env_slot = None if slots == n else _class_layout_slots(n, self.device)
             self.obs_buf = torch.empty((n, L.NUM_OBS), dtype=torch.float32, device=self.device)
             self.rew_buf = torch.empty(n, dtype=torch.float32, device=self.device)
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -164,16 +178,16 @@ class QuadVecTask:
         return self.num_observations
 
     def frows(self, f0, f1=None):
-        """Float fields [f0, f1) as a (k, N) tensor (a copy: the tiled layout has no flat row view)."""
+        """Float fields [f0, f1) as a (k, N) tensor in env order (a copy: the tiled layout has no flat row view)."""
         f1 = f0 + 1 if f1 is None else f1
         t = self.fstate[:, f0:f1, :].permute(1, 0, 2).reshape(f1 - f0, -1)
-        return t[:, :self.num_envs]
+        return t[:, :self.num_envs] if self._env_slot is None else t[:, self._env_slot]
 
     def irows(self, f0, f1=None):
-        """Int32 fields [f0, f1) as a (k, N) tensor (copy)."""
+        """Int32 fields [f0, f1) as a (k, N) tensor in env order (copy)."""
         f1 = f0 + 1 if f1 is None else f1
         t = self.istate[:, f0:f1, :].permute(1, 0, 2).reshape(f1 - f0, -1)
-        return t[:, :self.num_envs]
+        return t[:, :self.num_envs] if self._env_slot is None else t[:, self._env_slot]
 
     def set_frows(self, f0, values):
         """Write float fields [f0, f0 + k) of every env from a (k, N) tensor / array (the tiled counterpart of
@@ -192,7 +206,10 @@ class QuadVecTask:
         if n != self.num_envs or f0 < 0 or f0 + k > buf.shape[1]:
             raise ValueError(f"rows [{f0}, {f0 + k}) x {n} do not fit fields of {self.num_envs} envs")
         pad = torch.zeros((k, buf.shape[0] * L.TILE), dtype=dtype, device=self.device)
-        pad[:, :n] = v
+        if self._env_slot is None:
+            pad[:, :n] = v
+        else:
+            pad[:, self._env_slot] = v
         buf[:, f0:f0 + k, :] = pad.reshape(k, buf.shape[0], L.TILE).permute(1, 0, 2)
 
     def set_root_states(self, root13):
