@@ -255,6 +255,12 @@ __device__ __forceinline__ void dr_noise_apply(float* x, const ouz_dr_noise& p, 
   } else {                                                               // :629-633
     a = a * s + (1.0f - s); b = b * s + (1.0f - s); ac = ac * s + (1.0f - s); bc = bc * s + (1.0f - s);
   }
+  // Keep the correlated (step-independent) draws inside this rarely enabled branch: they are loop
+  // invariant in the fused rollout, and loop-invariant code motion hoisted them with their Box-Muller
+  // log / sincos out of the step loop and speculated them unconditionally, ~1500 instructions (~5000
+  // cycles) before the first step of every launch whether or not DR noise was on
+  // (scripts/stamp_rollout.py prologue, LeeLanded 8520 -> 3316 cycles).
+  __asm__ volatile("" : "+v"(gid));
 #pragma unroll
   for (int g = 0; g < (D + 3) / 4; ++g) {
     const U4 f = draw(seed, gid, step, stream, (uint32_t)g);

@@ -50,5 +50,8 @@ print(f"  last step: prelude+reset {np.median(st[:, 2] - last):.0f}, controller 
 if st[:, 12].any():
     print(f"  last step estimator: inputs->EKF {np.median(st[:, 10] - st[:, 2]):.0f}, EKF {np.median(st[:, 11] - st[:, 10]):.0f}, "
           f"PV {np.median(st[:, 12] - st[:, 11]):.0f}, guidance+Lee {np.median(st[:, 3] - st[:, 12]):.0f}")
+print(f"  prologue: state loads issued -> landed {np.median(st[:, 1] - st[:, 0]):.0f}, landed -> first step "
+      f"{np.median(st[:, 13] - st[:, 1]):.0f}; kernel entry (realtime) -> last wave exit "
+      f"{np.median([int(r[:, 9].max() - r[:, 8].min()) * 10 for r in rows]):.0f} ns")
 print(f"  launch: entry -> first step {np.median(st[:, 13] - st[:, 0]):.0f}, rollout {np.median(st[:, 29] - st[:, 13]):.0f}, "
       f"after last step -> stores landed {np.median(st[:, 7] - st[:, 29]):.0f}")
