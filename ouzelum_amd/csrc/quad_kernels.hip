@@ -234,7 +234,7 @@ __device__ __forceinline__ float normal_from(uint32_t a, uint32_t b, bool second
   const float u2 = unit_f32(b);
   const float r = sqrtf(-2.0f * logf(u1));
   float sn, cs;
-  sincosf(6.28318530717958647692f * u2, &sn, &cs);
+  sincospif(2.0f * u2, &sn, &cs);   // sin / cos(2 pi u2) with the exact reduction of sinpi (no Payne-Hanek code)
   return second ? r * sn : r * cs;
 }
 

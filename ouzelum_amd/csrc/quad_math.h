@@ -748,9 +748,9 @@ OUZ_HD void integrate_thrust_body(V3& p, Q4& q, V3& v, V3& w, const M3& R0, floa
       // exact in f32 there (the next terms are < 1e-8 relative)
       sc = 0.5f * h * (1.0f - th2 * (1.0f / 6.0f));
       co = 1.0f - 0.5f * th2 * (1.0f - th2 * (1.0f / 12.0f));
-    } else {
-      sc = sinf(th) / n;
-      co = cosf(th);
+    } else {   // only at other dt / sub-step settings (th <= h |w|max / 2): small arguments, no range reduction
+      sc = __sinf(th) / n;
+      co = __cosf(th);
     }
     q = quat_mul(q, Q4{wb.x * sc, wb.y * sc, wb.z * sc, co});
     // renormalise once, after the last sub-step: a product of unit quaternions stays unit to a few
