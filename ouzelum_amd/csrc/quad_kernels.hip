@@ -193,6 +193,17 @@ struct StepCtx {
   const float* actions;
 };
 
+// A copy of the RNG seed the compiler cannot treat as loop invariant, for draws in branches that are off
+// unless configured (DR noise): hoisted out of the fused rollout's step loop, their Philox round-key
+// schedules held SGPRs across the whole loop (spilled to VGPR lanes).  Not used for the reset / goal
+// draws: the RL tasks reset in some lane of most waves on most steps, and recomputing the key schedule
+// there cost QuadFault 12 % per step (6 080 -> 6 812 cycles).
+__device__ __forceinline__ uint64_t cold_seed(uint64_t seed) {
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32);
+  __asm__ volatile("" : "+s"(lo), "+s"(hi));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // ---------------------------------------------------------------------------
 // POMDP corruption (utils/POMDP.py:23-43) with counter-RNG draws
 // ---------------------------------------------------------------------------
@@ -261,6 +272,7 @@ __device__ __forceinline__ void dr_noise_apply(float* x, const ouz_dr_noise& p, 
   // cycles) before the first step of every launch whether or not DR noise was on
   // (scripts/stamp_rollout.py prologue, LeeLanded 8520 -> 3316 cycles).
   __asm__ volatile("" : "+v"(gid));
+  seed = cold_seed(seed);
 #pragma unroll
   for (int g = 0; g < (D + 3) / 4; ++g) {
     const U4 f = draw(seed, gid, step, stream, (uint32_t)g);
