@@ -87,3 +87,31 @@ def test_no_cpu_fallback():
     from ouzelum_amd._lib import OuzelumError
     with pytest.raises(OuzelumError):
         o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="cpu", rl_device="cpu")
+
+
+def test_state_slots_and_class_layout_map(L):
+    """ouz_state_slots (host-side, no GPU): the estimator tasks up to 64 K envs use the trigger-class layout
+    (blocks of 21 waves, one PV trigger class g % 21 per wave), every other task and size slot i = env i.
+    The Python slot map (vec_task._class_layout_slots) is the inverse of the kernel's slot -> env map."""
+    import numpy as np
+    import torch
+    from ouzelum_amd.vec_task import _class_layout_slots
+    est = (L.TASK_EKF_LEE_LANDED, L.TASK_TRACKING)
+    for task in range(L.NUM_TASKS):
+        for n in (1, 63, 64, 4096, 8192, 65536, 65537, 4194304):
+            want = ((n + 1343) // 1344) * 1344 if task in est and n <= 65536 else n
+            assert L.lib.ouz_state_slots(task, n) == want, (task, n)
+    assert L.lib.ouz_state_slots(99, 64) < 0 and L.lib.ouz_state_slots(0, 0) < 0
+    for n, off in ((4096, 0), (456 // 2, 456 // 2), (8192, 4096), (1000, 77)):
+        slot = _class_layout_slots(n, torch.device("cpu")).numpy()
+        slots = L.lib.ouz_state_slots(L.TASK_TRACKING, n)
+        assert len(set(slot.tolist())) == n and slot.max() < slots
+        env = np.full(slots, -1)
+        env[slot] = np.arange(n)
+        s = np.arange(slots)
+        b, r = s // 1344, s % 1344
+        np.testing.assert_array_equal(env[env >= 0], (b * 1344 + (r >> 6) + 21 * (r & 63))[env >= 0])
+        for w in range(slots // 64):                    # every wave holds one trigger class
+            e = env[w * 64:(w + 1) * 64]
+            e = e[e >= 0]
+            assert len({int(x) for x in (off + e) % 21}) <= 1
