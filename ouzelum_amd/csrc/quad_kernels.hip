@@ -858,7 +858,14 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
                                      float rew, bool rs, bool to, bool direct, bool keep_flags = false) {
   const uint32_t lane = (uint32_t)i & 63u;
   const uint32_t first = wave_tile(i) * 64u;   // wave-uniform: output bases live in SGPRs
+#if defined(OUZ_PROBE_EMIT) && OUZ_PROBE_EMIT == 1   // probe: no output stores at all
+  return;
+#endif
+#if defined(OUZ_PROBE_EMIT) && OUZ_PROBE_EMIT == 2   // probe: per-lane row stores at every size
+  if (!direct) {
+#else
   if (n <= kLatencyRegimeEnvs && !direct) {
+#endif
     // Latency regime (a few waves per CU, the step is one dependent chain): each lane stores its own
     // 52-byte row as three 16-byte stores + one dword (rows are 4-byte aligned; gfx950 global stores
     // take dword alignment), skipping the LDS round trip and the wave barrier of the staged form.
