@@ -1526,6 +1526,14 @@ struct ouz_env {
   double* wave_partials;     // [tiles][3] per-wave partials of the fused rollout statistics
   uint32_t* wave_ticket;     // their last-wave counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
+  // Whole-batch flicker coins of steps [mask_lo, mask_lo + kMaskCache): a pure function of (seed, task,
+  // step), drawn on the host (6 Philox blocks per step for a flickering task, ~0.3 us).  Filled for the
+  // next launch's steps right after a launch is submitted, while the GPU runs it, so a launch does not
+  // wait for its own coins (the first launch of a short timed region paid ~5 us of host time for them).
+  static constexpr int kMaskCache = 64;
+  int64_t mask_lo;
+  int32_t mask_n;
+  uint32_t mask[kMaskCache];
 };
 
 extern "C" {
@@ -1744,6 +1752,31 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 
+static uint32_t cached_flicker_mask(ouz_env* env, int64_t step) {
+  const int64_t off = step - env->mask_lo;
+  if (off >= 0 && off < env->mask_n) return env->mask[off];
+  return flicker_mask(env->args, env->cfg.task, (uint32_t)step);
+}
+
+// Coins of steps [from, from + count) into the cache (the window slides forward; count <= kMaskCache).
+static void prefill_flicker_masks(ouz_env* env, int64_t from, int count) {
+  if (from < env->mask_lo || from > env->mask_lo + env->mask_n) {   // not contiguous with the cached run: restart
+    env->mask_lo = from;
+    env->mask_n = 0;
+  }
+  const int64_t end = from + count;
+  if (end - env->mask_lo > ouz_env::kMaskCache) {   // slide: keep the tail still needed
+    const int64_t keep_lo = from;
+    const int drop = (int)(keep_lo - env->mask_lo);
+    const int kept = env->mask_n - drop > 0 ? env->mask_n - drop : 0;
+    for (int i = 0; i < kept; ++i) env->mask[i] = env->mask[i + drop];
+    env->mask_lo = keep_lo;
+    env->mask_n = kept;
+  }
+  for (int64_t st = env->mask_lo + env->mask_n; st < end; ++st)
+    env->mask[env->mask_n++] = flicker_mask(env->args, env->cfg.task, (uint32_t)st);
+}
+
 // Launch K (<= kMaxRolloutChunk) consecutive steps as ONE kernel.  K = 1 is VecTask.step.
 // ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
 // storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
@@ -1762,7 +1795,7 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
   for (int k = 0; k < K; ++k) {
     const uint32_t step = (uint32_t)(env->step + k);
     r.ctx[k].step = step;
-    r.ctx[k].flick_mask = flicker_mask(a, env->cfg.task, step);
+    r.ctx[k].flick_mask = cached_flicker_mask(env, env->step + k);
     r.ctx[k].actions = ring ? ring + (size_t)((ring_pos + k) % ring_len) * n * OUZ_NUM_ACT : nullptr;
   }
   dim3 g(grid_for(a.n_slots, blk)), b(blk);   // one lane per state slot
@@ -1780,6 +1813,7 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
 #undef OUZ_LAUNCH_TASK
   OUZ_LAUNCH_CHECK("quad_step_kernel");
   env->step += K;
+  prefill_flicker_masks(env, env->step, kMaxRolloutChunk);   // the next launch's coins, while this one runs
   return OUZ_OK;
 }
 
@@ -1855,7 +1889,7 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
   if (!wrench) return fail(OUZ_ERR_INVALID, "ouz_pre_physics: null wrench");
   const StepArgs& a = env->args;
   const int n = env->cfg.num_envs, blk = block_for(n);
-  StepCtx c{(uint32_t)env->step, flicker_mask(a, env->cfg.task, (uint32_t)env->step), actions};
+  StepCtx c{(uint32_t)env->step, cached_flicker_mask(env, env->step), actions};
   dim3 g(grid_for(a.n_slots, blk)), b(blk);
   hipStream_t s = (hipStream_t)stream;
   switch (env->cfg.task) {

@@ -19,6 +19,8 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--reps", type=int, default=30)
 ap.add_argument("--spin", action="store_true")
 ap.add_argument("--flags", type=int, default=None, help="hipSetDeviceFlags value (1 spin, 2 yield, 4 blocking)")
+ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each rep (GPU idle)")
+ap.add_argument("--pre-events", action="store_true", help="create and record the events once before each rep")
 a = ap.parse_args()
 if a.spin or a.flags is not None:
     hip = ctypes.CDLL("libamdhip64.so")
@@ -40,8 +42,13 @@ run.rollouts(5)
 run.prepare(a.steps)
 rows = []
 for _ in range(a.reps):
-    torch.cuda.synchronize(dev)
+    if a.idle_ms:
+        time.sleep(a.idle_ms * 1e-3)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if a.pre_events:
+        e0.record()
+        e1.record()
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     e0.record()
     run.rollouts(a.steps)
@@ -51,7 +58,7 @@ for _ in range(a.reps):
     t2 = time.perf_counter()
     rows.append((t1 - t0, t2 - t1, e0.elapsed_time(e1) * 1e-3))
 r = np.array(rows[3:]) * 1e6
-print(json.dumps({"steps": a.steps, "flags": a.flags if a.flags is not None else (1 if a.spin else None),
+print(json.dumps({"steps": a.steps, "idle_ms": a.idle_ms, "pre_events": a.pre_events, "flags": a.flags if a.flags is not None else (1 if a.spin else None),
                   "launch_host_us_median": round(float(np.median(r[:, 0])), 2),
                   "sync_host_us_median": round(float(np.median(r[:, 1])), 2),
                   "wall_us_median": round(float(np.median(r[:, 0] + r[:, 1])), 2),
