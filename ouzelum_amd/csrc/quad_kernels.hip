@@ -75,14 +75,14 @@ __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
     __builtin_amdgcn_sched_barrier(0);                                                           \
     if (wait) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                               \
     const uint64_t _t = __builtin_amdgcn_s_memtime();                                            \
-    const uint32_t _w = (uint32_t)i >> 6;   /* env index of the enclosing function */              \
+    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;   /* this wave's slot tile */  \
     if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
     __builtin_amdgcn_sched_barrier(0);                                                           \
   } while (0)
 #define OUZ_STAMP_RT(k)                                                                          \
   do {                                                                                           \
     const uint64_t _t = __builtin_amdgcn_s_memrealtime();                                        \
-    const uint32_t _w = (uint32_t)i >> 6;   /* env index of the enclosing function */              \
+    const uint32_t _w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;   /* this wave's slot tile */  \
     if ((threadIdx.x & 63) == 0 && _w < (uint32_t)kStampWaves) g_ouz_stamps[_w * kStampSlots + (k)] = _t; \
   } while (0)
 #else
