@@ -15,6 +15,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -32,6 +33,7 @@ constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS stagin
 // At or below this many envs a launch has at most 4 waves per CU and the step is latency-bound;
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
 constexpr int kLatencyRegimeEnvs = 65536;
+constexpr int kPipeTilesPerWave = 4;   // quad_step_pipe_kernel (large-N VecTask.step)
 // s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt / lgkmcnt left at their maxima (no wait)
 constexpr int kWaitVmcnt0 = (0x7 << 4) | (0xF << 8);
 
@@ -148,7 +150,8 @@ struct StepArgs {
   uint64_t n_total;
   uint64_t seed;
   int32_t track_episodes;
-  const ouz_dr_noise* drn;     // VecTask DR noise params in device memory: [0] observations, [1] actions
+  int32_t pipe_stride;         // quad_step_pipe_kernel: waves in its grid (0: that kernel is not used)
+  const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
   uint32_t* trace_resets;      // [trace_cap] envs reset at the start of each step
@@ -1211,6 +1214,86 @@ __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, Rol
   step_body<TASK, true, false, CLS>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
+// Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
+// smaller grid walks tiles t, t + stride, ...; before computing tile t it issues the state loads of tile
+// t + stride, so a wave keeps a load batch in flight while it computes instead of alternating load ->
+// compute -> store (the QuadFault step kernel at 4 M envs spends 47 % of its wave-cycles parked on memory
+// with 16 waves per CU: DESIGN.md §5).  Same per-env code as the VecTask.step path of run_env, so the
+// results are bitwise those of quad_step_kernel.  Tasks without the estimator only (the EKF's state is
+// 80 registers more: a second copy would cost the occupancy this buys).
+constexpr size_t kCtxArgOffset = (sizeof(StepArgs) + alignof(StepCtx) - 1) / alignof(StepCtx) * alignof(StepCtx);
+
+template <int CTRL, int TGT>
+__device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, const OutPtrs& o, float* wave_lds,
+                                          int t, int tiles, int task) {
+  const TaskParams& tp = a.tp[tp_slot(task)];
+  const int lane = (int)(threadIdx.x & 63u);
+  int i = t * 64 + lane;
+  bool valid = i < a.n;
+  EnvRegs<CTRL, TGT> S;
+  S.T = tile_of(a, i);
+  if (valid) env_load<CTRL, TGT>(a, i, tp, S, c.actions);
+  for (;;) {
+    // The argument blocks are re-read through laundered pointers every tile: otherwise the compiler
+    // hoists the wave-uniform float arithmetic on them (VALU results, held in VGPRs) out of the loop,
+    // ~80 registers that halved the occupancy.  The re-reads hit the scalar cache.
+    // (The kernel's arguments are (StepArgs, StepCtx) in that order at the start of the kernarg segment.)
+    const __attribute__((address_space(4))) char* kp =
+        (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+    __asm__ volatile("" : "+s"(kp));
+    const StepArgs& A = *(const StepArgs*)(const __attribute__((address_space(4))) StepArgs*)kp;
+    const StepCtx& C = *(const StepCtx*)(const __attribute__((address_space(4))) StepCtx*)(kp + kCtxArgOffset);
+    const TaskParams& TP = A.tp[tp_slot(task)];
+    const int tn = t + A.pipe_stride;   // wave-uniform: the loop exit and the next tile's bases stay scalar
+    const bool more = tn < tiles;
+    const int in = tn * 64 + lane;
+    const bool vn = more && in < A.n;
+    EnvRegs<CTRL, TGT> N;
+    N.T = tile_of(A, in);
+#ifndef OUZ_PIPE_NOPREF
+    if (vn) env_load<CTRL, TGT>(A, in, TP, N, C.actions);
+#endif
+    float ob[OUZ_NUM_OBS];
+    float rew = 0.0f;
+    bool rs = false, to = false;
+    const bool did_reset = valid && S.rst;
+    const bool flags_clear = valid && S.flags_clear;
+    if (valid) env_core<CTRL, TGT>(A, C, i, A.env_offset + (uint32_t)i, task, S, ob, rew, rs, to);
+    trace_count(A, C.step, did_reset, i, i);
+    emit(o, wave_lds, i, A.n, valid, ob, rew, rs, to, false, flags_clear);
+    if (valid) env_store<CTRL, TGT>(A, i, TP, S);
+    if (!more) break;
+#ifdef OUZ_PIPE_NOPREF
+    if (vn) env_load<CTRL, TGT>(A, in, TP, N, C.actions);
+#endif
+    S = N;
+    t = tn;
+    i = in;
+    valid = vn;
+  }
+}
+
+// Three waves per SIMD: unconstrained the loop takes 170 VGPRs (two waves); at four the allocator spills.
+#ifndef OUZ_PIPE_ATTR
+#define OUZ_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3, 3)))
+#endif
+__host__ __device__ constexpr bool pipe_task(int task) {
+  return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_LANDING;
+}
+
+template <int TASK>
+__global__ void __launch_bounds__(kMaxBlock) OUZ_PIPE_ATTR quad_step_pipe_kernel(StepArgs a, StepCtx c) {
+  prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
+  __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
+  float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
+  const OutPtrs o{a.obs, a.rew, a.reset, a.timeouts};
+  const int t = (int)__builtin_amdgcn_readfirstlane(blockIdx.x * (kMaxBlock / 64) + (threadIdx.x >> 6));
+  const int tiles = (a.n + 63) >> 6;
+  if (t >= tiles) return;
+  if constexpr (TASK == OUZ_TASK_LANDING) pipe_envs<CTRL_RL, TGT_TRAJ>(a, c, o, wave_lds, t, tiles, TASK);
+  else if constexpr (pipe_task(TASK)) pipe_envs<CTRL_RL, TGT_GOAL>(a, c, o, wave_lds, t, tiles, TASK);
+}
+
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
 __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;   // state slot
@@ -1649,6 +1732,17 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   a.n_total = (uint64_t)total;
   a.seed = cfg->seed;
   a.track_episodes = cfg->track_episodes;
+  a.pipe_stride = 0;
+  if (pipe_task(cfg->task) && cfg->num_envs > kLatencyRegimeEnvs) {
+    // tiles per wave of quad_step_pipe_kernel (OUZ_PIPE_TILES overrides; <= 1: the one-tile-per-wave kernel)
+    const char* pt = std::getenv("OUZ_PIPE_TILES");
+    const int per_wave = pt ? std::atoi(pt) : kPipeTilesPerWave;
+    if (per_wave > 1) {
+      const int tiles = (cfg->num_envs + 63) / 64, wpb = kMaxBlock / 64;
+      const int waves = (tiles + per_wave - 1) / per_wave;
+      a.pipe_stride = (waves + wpb - 1) / wpb * wpb;
+    }
+  }
   a.trace_env = -1;
   // x500 lumped mass properties (assets/x500/x500.urdf:31-35,98-177)
   const double base_m = 2.0, rm = 0.016076923076923075;
@@ -1741,6 +1835,13 @@ static uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
 // One task's step or rollout kernel; the estimator tasks have a trigger-class-layout instantiation.
 extern "C++" template <int T>
 static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, dim3 g, dim3 b, hipStream_t s) {
+  if constexpr (pipe_task(T)) {
+    if (single && a.pipe_stride) {
+      hipLaunchKernelGGL((quad_step_pipe_kernel<T>), dim3(a.pipe_stride / (kMaxBlock / 64)), dim3(kMaxBlock), 0, s,
+                         a, r.ctx[0]);
+      return;
+    }
+  }
   if constexpr (class_layout_task(T)) {
     if (a.cls) {
       if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g, b, 0, s, a, r.ctx[0]);

@@ -530,6 +530,41 @@ def test_large_n_matches_shards(ouz, task):
     assert torch.equal(full.obs_buf, torch.cat([h.obs_buf for h in halves], 0))
 
 
+@pytest.mark.parametrize("task", ["QuadFault", "Ouzelum", "Landing"])
+def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
+    """Above 65 536 envs the RL tasks' VecTask.step runs quad_step_pipe_kernel (4 tiles per wave, the next
+    tile's state loads in flight during this tile's compute); OUZ_PIPE_TILES=1 at env creation selects the
+    one-tile-per-wave quad_step_kernel.  Ragged size (a 37-lane last wave, a partial last stride) and a
+    sharded twin: state and outputs bit for bit equal over 30 steps with resets."""
+    from ouzelum_amd import _lib as L
+    n = 70016 + 37
+    envs = {}
+    for tiles in ("1", "4", "3"):
+        monkeypatch.setenv("OUZ_PIPE_TILES", tiles)
+        envs[tiles] = ouz.make(seed=13, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True)
+    monkeypatch.delenv("OUZ_PIPE_TILES")
+    shard = ouz.make(seed=13, task=task, num_envs=n - 66000, sim_device="cuda:0", env_id_offset=66000,
+                     num_envs_total=n, track_episodes=True)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    done = 0
+    for _ in range(30):
+        a = torch.rand((n, 4), device="cuda", generator=g) * 4 - 2
+        for e in envs.values():
+            e.step(a)
+        shard.step(a[66000:].contiguous())
+        done += int(envs["1"].reset_buf.sum())
+    torch.cuda.synchronize()
+    assert done > 0
+    ref = envs["1"]
+    for k in ("4", "3"):
+        assert torch.equal(envs[k].frows(0, L.F_COUNT), ref.frows(0, L.F_COUNT)), k
+        assert torch.equal(envs[k].irows(0, L.I_COUNT), ref.irows(0, L.I_COUNT)), k
+        for b in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+            assert torch.equal(getattr(envs[k], b), getattr(ref, b)), (k, b)
+    assert torch.equal(shard.frows(0, L.F_COUNT), ref.frows(0, L.F_COUNT)[:, 66000:])
+    assert torch.equal(shard.obs_buf, ref.obs_buf[66000:])
+
+
 @pytest.mark.parametrize("task,n", [("LeeLanded", 1), ("EKFLeeLanded", 63), ("QuadFault", 65), ("QuadTracking", 130),
                                     ("QuadMixed", 200), ("LeeLanded", 65537), ("QuadFault", 65537)])
 def test_ragged_sizes_parity(ouz, task, n):
