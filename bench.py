@@ -257,10 +257,11 @@ class Runner:
         self.rollouts(steps, fused)
         e1.record()
         torch.cuda.synchronize(dev)
-        gpu_us = e0.elapsed_time(e1) * 1e3 / steps
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        # after the clock stops: the process's first hipEventElapsedTime costs ~10 us of host time
+        gpu_us = e0.elapsed_time(e1) * 1e3 / steps
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

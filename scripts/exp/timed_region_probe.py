@@ -21,6 +21,8 @@ ap.add_argument("--spin", action="store_true")
 ap.add_argument("--flags", type=int, default=None, help="hipSetDeviceFlags value (1 spin, 2 yield, 4 blocking)")
 ap.add_argument("--idle-ms", type=float, default=0.0, help="host sleep before each rep (GPU idle)")
 ap.add_argument("--pre-events", action="store_true", help="create and record the events once before each rep")
+ap.add_argument("--settle", choices=["none", "sleep", "warm5"], default="none",
+                help="after the idle: a ~2 ms torch.cuda._sleep kernel, or a 5-step rollout, then synchronize")
 a = ap.parse_args()
 if a.spin or a.flags is not None:
     hip = ctypes.CDLL("libamdhip64.so")
@@ -44,6 +46,10 @@ rows = []
 for _ in range(a.reps):
     if a.idle_ms:
         time.sleep(a.idle_ms * 1e-3)
+    if a.settle == "sleep":
+        torch.cuda._sleep(int(4e6))
+    elif a.settle == "warm5":
+        run.rollouts(5)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if a.pre_events:
         e0.record()
@@ -58,7 +64,7 @@ for _ in range(a.reps):
     t2 = time.perf_counter()
     rows.append((t1 - t0, t2 - t1, e0.elapsed_time(e1) * 1e-3))
 r = np.array(rows[3:]) * 1e6
-print(json.dumps({"steps": a.steps, "idle_ms": a.idle_ms, "pre_events": a.pre_events, "flags": a.flags if a.flags is not None else (1 if a.spin else None),
+print(json.dumps({"steps": a.steps, "idle_ms": a.idle_ms, "settle": a.settle, "pre_events": a.pre_events, "flags": a.flags if a.flags is not None else (1 if a.spin else None),
                   "launch_host_us_median": round(float(np.median(r[:, 0])), 2),
                   "sync_host_us_median": round(float(np.median(r[:, 1])), 2),
                   "wall_us_median": round(float(np.median(r[:, 0] + r[:, 1])), 2),
