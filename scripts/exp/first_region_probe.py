@@ -17,6 +17,8 @@ ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--zero-storage", action="store_true")
 ap.add_argument("--prep-first", action="store_true")
 ap.add_argument("--mode", choices=["inline", "timed", "timed-nogc"], default="inline")
+ap.add_argument("--sync", choices=["device", "event", "stream", "query"], default="device",
+                help="inline mode: wait for e1 this way before torch.cuda.synchronize()")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -70,9 +72,16 @@ for _ in range(6):
     tc = time.perf_counter()
     e1.record()
     td = time.perf_counter()
+    if a.sync == "event":
+        e1.synchronize()
+    elif a.sync == "stream":
+        torch.cuda.current_stream(dev).synchronize()
+    elif a.sync == "query":
+        while not e1.query():
+            pass
     torch.cuda.synchronize(dev)
     te = time.perf_counter()
     us = [round((x - t0) * 1e6, 1) for x in (ta, tb, tc, td, te)]
     res.append({"e0_rec": us[0], "after_l16": us[1], "after_l4": us[2], "e1_rec": us[3], "wall": us[4],
                 "gpu": round(e0.elapsed_time(e1) * 1e3, 1)})
-print(json.dumps({"zero_storage": a.zero_storage, "prep_first": a.prep_first, "regions": res}), flush=True)
+print(json.dumps({"sync": a.sync, "zero_storage": a.zero_storage, "prep_first": a.prep_first, "regions": res}), flush=True)
