@@ -16,12 +16,18 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--zero-storage", action="store_true")
 ap.add_argument("--prep-first", action="store_true")
+ap.add_argument("--flags", type=int, default=None, help="hipSetDeviceFlags (1 spin, 2 yield, 4 blocking)")
 ap.add_argument("--mode", choices=["inline", "timed", "timed-nogc"], default="inline")
 ap.add_argument("--sync", choices=["device", "event", "stream", "query"], default="device",
                 help="inline mode: wait for e1 this way before torch.cuda.synchronize()")
 a = ap.parse_args()
 
 import torch  # noqa: E402
+
+if a.flags is not None:   # torch's own libamdhip64 (the one the process runs on), before the device starts
+    import ctypes
+    hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+    print("hipSetDeviceFlags", a.flags, "rc", hip.hipSetDeviceFlags(ctypes.c_uint(a.flags)), file=sys.stderr)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import bench as B  # noqa: E402
@@ -49,7 +55,7 @@ if a.mode != "inline":
         el, gpu_us = run.timed(a.steps, 1)
         gc.enable()
         res.append({"wall": round(el * 1e6, 1), "gpu": round(gpu_us * a.steps, 1)})
-    print(json.dumps({"mode": a.mode, "regions": res}), flush=True)
+    print(json.dumps({"flags": a.flags, "mode": a.mode, "regions": res}), flush=True)
     sys.exit(0)
 for _ in range(6):
     # Runner.timed with host timestamps after each launch call and before the final synchronize
@@ -84,4 +90,4 @@ for _ in range(6):
     us = [round((x - t0) * 1e6, 1) for x in (ta, tb, tc, td, te)]
     res.append({"e0_rec": us[0], "after_l16": us[1], "after_l4": us[2], "e1_rec": us[3], "wall": us[4],
                 "gpu": round(e0.elapsed_time(e1) * 1e3, 1)})
-print(json.dumps({"sync": a.sync, "zero_storage": a.zero_storage, "prep_first": a.prep_first, "regions": res}), flush=True)
+print(json.dumps({"flags": a.flags, "sync": a.sync, "zero_storage": a.zero_storage, "prep_first": a.prep_first, "regions": res}), flush=True)
