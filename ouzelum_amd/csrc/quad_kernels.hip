@@ -840,20 +840,23 @@ struct OutPtrs {
 };
 
 // One lane's outputs by env index e (the trigger-class layout: a wave's envs are 21 apart): the 52-byte obs
-// row as three 16-byte stores + one dword, reward / flags at [e].
+// row as three 16-byte stores + one dword, reward / flags at [e].  Plain (temporal) stores: the lanes of
+// a wave write partial lines 21 envs apart, which the L2 merges with the other class waves' writes to the
+// same lines; as non-temporal stores they reached memory as partial writes (QuadTracking 4096 fused step
+// 5.23 -> 4.99 us, per-step kernel 8.7 -> 7.6 us with plain stores; profiles/r02/temporal_*).
 __device__ __forceinline__ void emit_env(const OutPtrs& o, int e, bool valid, const float* ob, float rew, bool rs,
                                          bool to, bool keep_flags) {
   if (!valid) return;
   typedef float f4a4 __attribute__((ext_vector_type(4), aligned(4)));
   float* row = o.obs + (size_t)e * OUZ_NUM_OBS;
-  OUZ_ST(reinterpret_cast<f4a4*>(row), (f4a4{ob[0], ob[1], ob[2], ob[3]}));
-  OUZ_ST(reinterpret_cast<f4a4*>(row + 4), (f4a4{ob[4], ob[5], ob[6], ob[7]}));
-  OUZ_ST(reinterpret_cast<f4a4*>(row + 8), (f4a4{ob[8], ob[9], ob[10], ob[11]}));
-  OUZ_ST(&row[12], ob[12]);
-  OUZ_ST(&o.rew[e], rew);
+  *reinterpret_cast<f4a4*>(row) = f4a4{ob[0], ob[1], ob[2], ob[3]};
+  *reinterpret_cast<f4a4*>(row + 4) = f4a4{ob[4], ob[5], ob[6], ob[7]};
+  *reinterpret_cast<f4a4*>(row + 8) = f4a4{ob[8], ob[9], ob[10], ob[11]};
+  row[12] = ob[12];
+  o.rew[e] = rew;
   if (!(keep_flags && !rs)) {
-    OUZ_ST(&o.reset[e], (int64_t)(rs ? 1 : 0));
-    OUZ_ST(&o.timeouts[e], (uint8_t)(to ? 1 : 0));
+    o.reset[e] = rs ? 1 : 0;
+    o.timeouts[e] = to ? 1 : 0;
   }
 }
 
