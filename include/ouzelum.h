@@ -52,7 +52,8 @@
 extern "C" {
 #endif
 
-#define OUZ_ABI_VERSION 2   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots) */
+#define OUZ_ABI_VERSION 3   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
+                               3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots */
 
 /* error codes */
 #define OUZ_OK 0
@@ -66,7 +67,7 @@ extern "C" {
 #define OUZ_TASK_EKF_LEE_LANDED 2 /* AHRS-EKF + PV-KF + Lee (tasks/ekf_lee_landed.py)                    */
 #define OUZ_TASK_TRACKING 3       /* EKF pipeline + trajectory platform + DR                    config C */
 #define OUZ_TASK_FAULT 4          /* RL thrust + single-rotor fault + obs noise                 config D */
-#define OUZ_TASK_MIXED 5          /* per-64-env curriculum of tasks 1/3/4                       config E */
+#define OUZ_TASK_MIXED 5          /* curriculum of tasks 1/3/4 per OUZ_MIXED_CHUNK global ids   config E */
 #define OUZ_TASK_LANDING 6        /* RL thrust, land on the husky following its trajectories (tasks/landing.py);
                                      the reference learners' default env (RPO-LSTM/main.py:18)              */
 #define OUZ_NUM_TASKS 7
@@ -105,7 +106,15 @@ extern "C" {
  * rounded up to a multiple of 1344; padding slots stay zero.  Slot of env e:
  * b*1344 + (r % 21)*64 + r/21 with b = e/1344, r = e - b*1344.  Buffers must
  * hold OUZ_TILED_SIZE(ouz_state_slots(task, num_envs), count) elements.  The
- * env-order buffers (obs, rew, reset, time_outs, actions) are indexed by env. */
+ * env-order buffers (obs, rew, reset, time_outs, actions) are indexed by env.
+ * OUZ_TASK_MIXED assigns LeeLanded / QuadTracking / QuadFault to consecutive
+ * chunks of OUZ_MIXED_CHUNK (= 1344, one class block) global ids; up to 65536
+ * envs its slot space is chunk-aligned in global ids (slot s holds global id
+ * c*1344 + r' with c = env_id_offset/1344 + s/1344, r = s % 1344, r' the class
+ * permutation above in a QuadTracking chunk and r elsewhere; ids outside the
+ * shard are idle slots), ouz_state_slots = (ceil(num_envs/1344) + 1) * 1344.
+ * ouz_env_slots gives every env's slot for any task, size and offset. */
+#define OUZ_MIXED_CHUNK 1344
 #define OUZ_TILE 64
 #define OUZ_TILES(n) (((n) + OUZ_TILE - 1) / OUZ_TILE)
 #define OUZ_TILED_SIZE(n, count) ((size_t)OUZ_TILES(n) * (count) * OUZ_TILE)
@@ -213,6 +222,9 @@ typedef struct ouz_env ouz_env;
 int32_t ouz_abi_version(void);
 /* State slots of a task at num_envs (see "State slots" above); negative on bad arguments. */
 int64_t ouz_state_slots(int32_t task, int32_t num_envs);
+/* State slot of each of num_envs envs of a shard starting at global id env_id_offset, into the host
+ * array env_slot[num_envs] (host-side, no GPU; the inverse of the kernels' slot -> env map). */
+int ouz_env_slots(int32_t task, int32_t num_envs, int64_t env_id_offset, int32_t* env_slot);
 const char* ouz_last_error(void);
 void ouz_default_config(ouz_config* cfg);
 int ouz_task_info_get(int32_t task, ouz_task_info* out);

@@ -603,7 +603,7 @@ TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, T
 TASK_NAMES = {"Ouzelum": TASK_OUZELUM, "LeeLanded": TASK_LEE_LANDED, "EKFLeeLanded": TASK_EKF_LEE_LANDED,
               "QuadTracking": TASK_TRACKING, "QuadFault": TASK_FAULT, "QuadMixed": TASK_MIXED,
               "Landing": TASK_LANDING}
-MIXED_CHUNK = 64                       # envs per task block in the mixed curriculum (one wave)
+MIXED_CHUNK = 1344                     # global ids per task chunk of the mixed curriculum (21 waves)
 MIXED_TASKS = (TASK_LEE_LANDED, TASK_TRACKING, TASK_FAULT)
 
 

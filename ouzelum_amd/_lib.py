@@ -22,14 +22,14 @@ class OuzelumError(RuntimeError):
 
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
-ABI_VERSION = 2
+ABI_VERSION = 3
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
 LEE_POSITION, LEE_VELOCITY, LEE_ATTITUDE = range(3)
 NUM_OBS, NUM_ACT = 13, 4
 TGT_GOAL, TGT_PLATFORM, TGT_TRAJ = range(3)
-MIXED_CHUNK = 64
+MIXED_CHUNK = 1344
 MIXED_TASKS = (TASK_LEE_LANDED, TASK_TRACKING, TASK_FAULT)
 F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
 F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
@@ -84,6 +84,7 @@ _I64 = ctypes.c_int64
 SIGNATURES = {
     "ouz_abi_version": (_I, []),
     "ouz_state_slots": (_I64, [_I, _I]),
+    "ouz_env_slots": (_I, [_I, _I, _I64, _P]),
     "ouz_last_error": (ctypes.c_char_p, []),
     "ouz_default_config": (None, [ctypes.POINTER(OuzConfig)]),
     "ouz_task_info_get": (_I, [_I, ctypes.POINTER(OuzTaskInfo)]),

@@ -28,7 +28,6 @@ namespace ouz {
 
 enum Ctrl { CTRL_RL = 0, CTRL_LEE_TRUE = 1, CTRL_LEE_EST = 2 };
 enum TargetMode { TGT_GOAL = 0, TGT_PLATFORM = 1, TGT_TRAJ = 2 };
-constexpr int kMixedChunk = 64;
 constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS staging is sized for it)
 // At or below this many envs a launch has at most 4 waves per CU and the step is latency-bound;
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
@@ -49,22 +48,47 @@ constexpr int kClassBlock = kTrigClasses * 64;
 // Latency regime only: at large N the env-order buffers' per-lane accesses 21 envs apart would cost more
 // HBM traffic (a 64-byte line per lane for the 8-byte reset flag, measured 0.74 -> 0.30 of HBM peak at
 // 4 M envs) than the uniform triggers save; there the step is HBM-bound and keeps slot i = env i.
+// The mixed curriculum (config E) assigns tasks to chunks of 1344 global ids (LeeLanded, QuadTracking,
+// QuadFault, repeating): a chunk is one class block, so in the latency regime its QuadTracking chunks take
+// the trigger-class layout too.  Its slot space is chunk-aligned in global ids: slot s of a shard holds
+// global id c*1344 + r' with c = env_offset/1344 + s/1344, r = s % 1344 and r' = the class permutation of
+// r in a QuadTracking chunk, r' = r otherwise; ids outside the shard are idle slots.  At most
+// ceil(n/1344) + 1 chunks touch a shard of n envs.
+constexpr int kMixedChunk = kClassBlock;
+__host__ __device__ constexpr int mixed_chunk_task(uint32_t chunk) {
+  return chunk % 3u == 0u ? OUZ_TASK_LEE_LANDED : (chunk % 3u == 1u ? OUZ_TASK_TRACKING : OUZ_TASK_FAULT);
+}
 __host__ __device__ constexpr bool class_layout_task(int task) {
-  return task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING;
+  return task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING || task == OUZ_TASK_MIXED;
 }
 __host__ __device__ constexpr bool class_layout(int task, int n) {
   return class_layout_task(task) && n <= kLatencyRegimeEnvs;
 }
 __host__ __device__ inline int state_slots(int task, int n) {
-  return class_layout(task, n) ? ((n + kClassBlock - 1) / kClassBlock) * kClassBlock : n;
+  if (!class_layout(task, n)) return n;
+  const int blocks = (n + kClassBlock - 1) / kClassBlock;
+  return (task == OUZ_TASK_MIXED ? blocks + 1 : blocks) * kClassBlock;
 }
 __host__ __device__ inline int slot_env(int s) {   // class layout: env held by state slot s
   const int b = s / kClassBlock, r = s - b * kClassBlock;
   return b * kClassBlock + (r >> 6) + kTrigClasses * (r & 63);
 }
-__host__ __device__ inline int env_slot(int e) {   // its inverse
+__host__ __device__ inline int env_slot_of(int e) {   // its inverse
   const int b = e / kClassBlock, r = e - b * kClassBlock;
   return b * kClassBlock + (r % kTrigClasses) * 64 + r / kTrigClasses;
+}
+// Mixed curriculum, latency regime: the env (shard-local index; < 0 or >= n: an idle slot) held by slot s.
+__host__ __device__ inline int64_t mixed_slot_env(uint32_t env_offset, int s) {
+  const uint32_t c = env_offset / kClassBlock + (uint32_t)(s / kClassBlock);
+  const int r = s % kClassBlock;
+  const int rel = mixed_chunk_task(c) == OUZ_TASK_TRACKING ? (r >> 6) + kTrigClasses * (r & 63) : r;
+  return (int64_t)c * kClassBlock + rel - (int64_t)env_offset;
+}
+__host__ inline int mixed_env_slot(uint32_t env_offset, int e) {   // its inverse
+  const uint32_t gid = env_offset + (uint32_t)e, c = gid / kClassBlock;
+  const int r = (int)(gid % kClassBlock);
+  const int rel = mixed_chunk_task(c) == OUZ_TASK_TRACKING ? (r % kTrigClasses) * 64 + r / kTrigClasses : r;
+  return (int)(c - env_offset / kClassBlock) * kClassBlock + rel;
 }
 
 // Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
@@ -145,7 +169,7 @@ struct StepArgs {
   const float2* wp_tab;        // lemniscate[100] | circle[100] | square[4]
   int32_t n;
   int32_t n_slots;             // state slots: n, or the trigger-class layout's padded count
-  int32_t cls;                 // 1: trigger-class slot layout (estimator tasks)
+  int32_t cls;                 // 1: trigger-class slot layout (estimator tasks), 2: the mixed curriculum's
   uint32_t env_offset;
   uint64_t n_total;
   uint64_t seed;
@@ -183,10 +207,7 @@ __device__ __forceinline__ float map_to_pi(float a) {   // utils/controllers.py:
 constexpr int kTrajLen[3] = {100, 100, 4};
 constexpr int kTrajBase[3] = {0, 100, 200};
 
-__device__ __forceinline__ int mixed_task(uint32_t gid) {
-  const int tasks[3] = {OUZ_TASK_LEE_LANDED, OUZ_TASK_TRACKING, OUZ_TASK_FAULT};
-  return tasks[(gid / kMixedChunk) % 3];
-}
+__device__ __forceinline__ int mixed_task(uint32_t gid) { return mixed_chunk_task(gid / kMixedChunk); }
 
 // Per-step context: the step counter (keys every draw, drives the convergence window),
 // the host-drawn whole-batch flicker coins and this step's action batch.
@@ -386,9 +407,13 @@ struct EnvRegs {
 };
 
 // One env's action row (vec_task.py:313: actions (N, 4) f32 on rl_device): a 16-byte load per lane.
-template <int CTRL, int TGT>
-__device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL, TGT>& S) {
-  if constexpr (CTRL == CTRL_RL) S.act = reinterpret_cast<const float4*>(actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
+// CLS: the slot layout is not env order (the mixed curriculum's class layout): the row of env e.
+template <int CTRL, int TGT, bool CLS = false>
+__device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL, TGT>& S, int e = 0) {
+  if constexpr (CTRL == CTRL_RL) {
+    if constexpr (CLS) S.act = reinterpret_cast<const float4*>(actions)[e];
+    else S.act = reinterpret_cast<const float4*>(actions + (size_t)S.T.first * OUZ_NUM_ACT)[S.T.l];
+  }
 }
 
 template <int CTRL, int TGT, bool CLS = false>
@@ -428,7 +453,7 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
     if (tp.fault) { S.frot = ldi(S.T, OUZ_I_FAULT_ROTOR); S.fonset = ldi(S.T, OUZ_I_FAULT_ONSET); S.eta = ld(S.T, OUZ_F_FAULT_ETA); }
     // in flight with the state loads: issued inside the step it would be a second memory round trip
     // behind the reset branch (every wave's critical path, and half the bytes in flight at large N)
-    load_actions<CTRL, TGT>(actions, S);
+    load_actions<CTRL, TGT, CLS>(actions, S, i);
   }
   if constexpr (CTRL == CTRL_LEE_EST) {
     S.prev_v = ld3(S.T, OUZ_F_PREV_V);
@@ -1016,7 +1041,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
       if (valid) env_core<CTRL, TGT>(a, ctx[k], e, gid, task, S, ob, rew, rs, to);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
-      if (valid && k + 1 < K) load_actions<CTRL, TGT>(ctx[k + 1].actions, S);   // next step's row, before emit
+      if (valid && k + 1 < K) load_actions<CTRL, TGT, CLS>(ctx[k + 1].actions, S, e);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i, e);
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
@@ -1158,7 +1183,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
   const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
   const int first = i - (int)(threadIdx.x & 63);
   if (first >= (CLS ? a.n_slots : a.n)) return;   // whole wave past the end
-  const int e = CLS ? slot_env(i) : i;             // env index
+  int e = i;                                       // env index (a.n: an idle slot)
+  if constexpr (CLS && TASK == OUZ_TASK_MIXED) {
+    const int64_t e64 = mixed_slot_env(a.env_offset, i);
+    e = (e64 >= 0 && e64 < a.n) ? (int)e64 : a.n;
+  } else if constexpr (CLS) {
+    e = slot_env(i);
+  }
   const bool valid = e < a.n;
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
@@ -1172,6 +1203,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
     run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+  } else if constexpr (CLS) {
+    // mixed curriculum, class layout: a wave's slots lie in one 1344-id chunk, so its task is wave-uniform
+    const uint32_t c = a.env_offset / kClassBlock + __builtin_amdgcn_readfirstlane((uint32_t)first) / kClassBlock;
+    const int t = mixed_chunk_task(c);
+    if (t == OUZ_TASK_LEE_LANDED)
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                           OUZ_TASK_LEE_LANDED, false, sm, &ls, wrench);
+    else if (t == OUZ_TASK_TRACKING)
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                      OUZ_TASK_TRACKING, false, sm, &ls, wrench);
+    else
+      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_FAULT,
+                                                 false, sm, &ls, wrench);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -1303,8 +1347,9 @@ __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   if (s >= a.n_slots) return;
   for (int k = 0; k < OUZ_F_COUNT; ++k) st(a, k, s, 0.0f);
   for (int k = 0; k < OUZ_I_COUNT; ++k) sti(a, k, s, 0);
-  const int e = a.cls ? slot_env(s) : s;                 // env index (padding slots stay zero)
-  if (e >= a.n) return;
+  // env index (padding / idle slots stay zero)
+  const int64_t e = a.cls == 2 ? mixed_slot_env(a.env_offset, s) : (a.cls ? slot_env(s) : s);
+  if (e < 0 || e >= a.n) return;
   const uint32_t gid = a.env_offset + (uint32_t)e;
   const int task = task_cfg == OUZ_TASK_MIXED ? mixed_task(gid) : task_cfg;
   const TaskParams& tp = a.tp[tp_slot(task)];
@@ -1637,6 +1682,15 @@ int64_t ouz_state_slots(int32_t task, int32_t num_envs) {
   if (task < 0 || task >= OUZ_NUM_TASKS || num_envs <= 0) return fail(OUZ_ERR_INVALID, "ouz_state_slots: bad task / size");
   return state_slots(task, num_envs);
 }
+int ouz_env_slots(int32_t task, int32_t num_envs, int64_t env_id_offset, int32_t* env_slot) {
+  if (task < 0 || task >= OUZ_NUM_TASKS || num_envs <= 0 || !env_slot || env_id_offset < 0 ||
+      env_id_offset + num_envs > 0xFFFFFFFFll)
+    return fail(OUZ_ERR_INVALID, "ouz_env_slots: bad arguments");
+  const bool cls = class_layout(task, num_envs);
+  for (int32_t e = 0; e < num_envs; ++e)
+    env_slot[e] = !cls ? e : (task == OUZ_TASK_MIXED ? mixed_env_slot((uint32_t)env_id_offset, e) : env_slot_of(e));
+  return OUZ_OK;
+}
 const char* ouz_last_error(void) { return g_err.c_str(); }
 
 void ouz_default_config(ouz_config* c) {
@@ -1730,7 +1784,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   a.wp_tab = e->wp_tab;
   a.n = cfg->num_envs;
   a.n_slots = state_slots(cfg->task, cfg->num_envs);
-  a.cls = class_layout(cfg->task, cfg->num_envs) ? 1 : 0;
+  a.cls = class_layout(cfg->task, cfg->num_envs) ? (cfg->task == OUZ_TASK_MIXED ? 2 : 1) : 0;
   a.env_offset = (uint32_t)cfg->env_id_offset;
   a.n_total = (uint64_t)total;
   a.seed = cfg->seed;
@@ -2009,7 +2063,10 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
       break;
     case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LANDING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LANDING>, g, b, 0, s, a, c, wrench); break;
-    default: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_MIXED>, g, b, 0, s, a, c, wrench); break;
+    default:
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true>), g, b, 0, s, a, c, wrench);
+      else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, false>), g, b, 0, s, a, c, wrench);
+      break;
   }
   OUZ_LAUNCH_CHECK("quad_pre_kernel");
   return OUZ_OK;

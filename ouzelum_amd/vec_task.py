@@ -41,12 +41,12 @@ def task_info(task: int) -> L.OuzTaskInfo:
     return info
 
 
-def _class_layout_slots(n, device):
-    """State slot of each env under the trigger-class layout (include/ouzelum.h "State slots"; estimator tasks
-    up to 65536 envs): blocks of 1344 slots, tile k of block b holds envs b*1344 + k + 21*lane."""
-    e = torch.arange(n, device=device, dtype=torch.int64)
-    b, r = e // 1344, e % 1344
-    return b * 1344 + (r % 21) * 64 + r // 21
+def env_slots(task, n, env_id_offset=0):
+    """State slot of each env (``ouz_env_slots``: include/ouzelum.h "State slots"; the estimator tasks and the
+    mixed curriculum up to 65536 envs group envs by PV trigger class), as an int64 numpy array."""
+    out = np.empty(int(n), dtype=np.int32)
+    L.check(L.lib.ouz_env_slots(int(task), int(n), int(env_id_offset), out.ctypes.data), "ouz_env_slots")
+    return out.astype(np.int64)
 
 
 class QuadVecTask:
@@ -119,7 +119,8 @@ class QuadVecTask:
             self.fstate = torch.zeros((L.tiles(slots), L.F_COUNT, L.TILE), dtype=torch.float32, device=self.device)
             self.istate = torch.zeros((L.tiles(slots), L.I_COUNT, L.TILE), dtype=torch.int32, device=self.device)
             # env -> state slot (None: slot i is env i)
-            self._env_slot = None if slots == n else _class_layout_slots(n, self.device)
+            self._env_slot = (None if slots == n else
+                              torch.from_numpy(env_slots(self.task, n, cfg.env_id_offset)).to(self.device))
             self.obs_buf = torch.empty((n, L.NUM_OBS), dtype=torch.float32, device=self.device)
             self.rew_buf = torch.empty(n, dtype=torch.float32, device=self.device)
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)
@@ -239,7 +240,7 @@ class QuadVecTask:
         return self.frows(0, 13).t()
 
     def env_task_ids(self):
-        """Per-env task id (the mixed curriculum assigns tasks per 64-env block of global ids)."""
+        """Per-env task id (the mixed curriculum assigns tasks per chunk of L.MIXED_CHUNK global ids)."""
         gid = torch.arange(self.num_envs, device=self.device) + int(self.cfg.env_id_offset)
         if self.task != L.TASK_MIXED:
             return torch.full_like(gid, self.task)

@@ -29,6 +29,7 @@ def global_ring(total, seed):
 def main():
     out_dir, task, n, rollouts, seed = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
     from ouzelum_amd import make
+    from ouzelum_amd import _lib as L
     from ouzelum_amd.distributed import ReturnAllReduce, init_from_env
     rank, world, local = init_from_env()
     dev = torch.device("cuda", local)
@@ -48,8 +49,8 @@ def main():
     red.finish()
     rows = torch.stack([red.result(r).clone() for r in range(rollouts)])
     torch.cuda.synchronize(dev)
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), fstate=env.fstate.cpu().numpy(),
-             istate=env.istate.cpu().numpy(), root=env.root_states.cpu().numpy(), obs=storage[0].cpu().numpy(), rew=storage[1].cpu().numpy(),
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), fstate=env.frows(0, L.F_COUNT).cpu().numpy(),
+             istate=env.irows(0, L.I_COUNT).cpu().numpy(), root=env.root_states.cpu().numpy(), obs=storage[0].cpu().numpy(), rew=storage[1].cpu().numpy(),
              reduced=rows.cpu().numpy(), step=env.sim_step_count)
     import torch.distributed as dist
     dist.barrier()

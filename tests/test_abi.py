@@ -90,28 +90,62 @@ def test_no_cpu_fallback():
 
 
 def test_state_slots_and_class_layout_map(L):
-    """ouz_state_slots (host-side, no GPU): the estimator tasks up to 64 K envs use the trigger-class layout
-    (blocks of 21 waves, one PV trigger class g % 21 per wave), every other task and size slot i = env i.
-    The Python slot map (vec_task._class_layout_slots) is the inverse of the kernel's slot -> env map."""
+    """ouz_state_slots / ouz_env_slots (host-side, no GPU): the estimator tasks and the mixed curriculum up to
+    64 K envs use the trigger-class layout (blocks of 21 waves, one PV trigger class g % 21 per wave; the
+    mixed curriculum's slot space chunk-aligned in global ids, one 1344-id task chunk per 21 waves), every
+    other task and size slot i = env i.  The env -> slot map is checked against the kernels' slot -> env
+    formulas restated here."""
     import numpy as np
-    import torch
-    from ouzelum_amd.vec_task import _class_layout_slots
+    from ouzelum_amd.vec_task import env_slots
     est = (L.TASK_EKF_LEE_LANDED, L.TASK_TRACKING)
     for task in range(L.NUM_TASKS):
         for n in (1, 63, 64, 4096, 8192, 65536, 65537, 4194304):
-            want = ((n + 1343) // 1344) * 1344 if task in est and n <= 65536 else n
+            if task in est and n <= 65536:
+                want = ((n + 1343) // 1344) * 1344
+            elif task == L.TASK_MIXED and n <= 65536:
+                want = ((n + 1343) // 1344 + 1) * 1344
+            else:
+                want = n
             assert L.lib.ouz_state_slots(task, n) == want, (task, n)
     assert L.lib.ouz_state_slots(99, 64) < 0 and L.lib.ouz_state_slots(0, 0) < 0
-    for n, off in ((4096, 0), (456 // 2, 456 // 2), (8192, 4096), (1000, 77)):
-        slot = _class_layout_slots(n, torch.device("cpu")).numpy()
-        slots = L.lib.ouz_state_slots(L.TASK_TRACKING, n)
-        assert len(set(slot.tolist())) == n and slot.max() < slots
-        env = np.full(slots, -1)
-        env[slot] = np.arange(n)
-        s = np.arange(slots)
-        b, r = s // 1344, s % 1344
-        np.testing.assert_array_equal(env[env >= 0], (b * 1344 + (r >> 6) + 21 * (r & 63))[env >= 0])
-        for w in range(slots // 64):                    # every wave holds one trigger class
-            e = env[w * 64:(w + 1) * 64]
-            e = e[e >= 0]
-            assert len({int(x) for x in (off + e) % 21}) <= 1
+    assert L.MIXED_CHUNK == 1344
+    for task in (L.TASK_TRACKING, L.TASK_MIXED, L.TASK_FAULT):
+        for n, off in ((4096, 0), (456 // 2, 456 // 2), (4096, 4096), (8192, 4096), (1000, 77), (4096, 28672),
+                       (65536, 1344 * 5 + 3), (70000, 64)):
+            slot = env_slots(task, n, off)
+            slots = L.lib.ouz_state_slots(task, n)
+            assert len(set(slot.tolist())) == n and slot.min() >= 0 and slot.max() < slots, (task, n, off)
+            env = np.full(slots + 63, -1)
+            env[slot] = np.arange(n)
+            s = np.arange(slots)
+            if slots == n:
+                np.testing.assert_array_equal(slot, np.arange(n))
+                continue
+            r = s % 1344
+            perm = (r >> 6) + 21 * (r & 63)
+            if task == L.TASK_MIXED:      # chunk-aligned in global ids
+                c = off // 1344 + s // 1344
+                gid = c * 1344 + np.where(c % 3 == 1, perm, r)
+                e_of_s = gid - off
+            else:                         # blocks of the shard's own env index
+                e_of_s = (s // 1344) * 1344 + perm
+            ok = env[:slots] >= 0
+            np.testing.assert_array_equal(env[:slots][ok], e_of_s[ok])
+            assert not np.any((e_of_s >= 0) & (e_of_s < n) & ~ok)     # every in-range id has its slot
+            for w in range(slots // 64):
+                e = env[w * 64:(w + 1) * 64]
+                e = e[e >= 0]
+                if len(e) == 0:
+                    continue
+                gid = off + e
+                tasks = {int(x) for x in (gid // 1344) % 3} if task == L.TASK_MIXED else {1}
+                assert len(tasks) == 1                                  # one chunk task per wave
+                if task == L.TASK_TRACKING or tasks == {1}:
+                    cls = (gid if task == L.TASK_MIXED else e + off) % 21
+                    assert len({int(x) for x in cls}) == 1              # one trigger class per wave
+                else:
+                    assert np.all(np.diff(e) == 1)                      # identity chunks: consecutive envs
+    bad = np.empty(4, dtype=np.int32)
+    assert L.lib.ouz_env_slots(L.TASK_MIXED, 4, -1, bad.ctypes.data) < 0
+
+

@@ -82,9 +82,13 @@ def test_two_rank_hip_shards_match_single_process(tmp_path, task, n, rollouts):
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
     assert all(int(p["step"]) == full.sim_step_count for p in parts)
     np.testing.assert_array_equal(np.concatenate([p["root"] for p in parts]), full.root_states.cpu().numpy())
-    if n % 64 == 0:   # the shards' wave tiles line up with the unsharded tiles: the whole state, every field
-        np.testing.assert_array_equal(np.concatenate([p["fstate"] for p in parts]), full.fstate.cpu().numpy())
-        np.testing.assert_array_equal(np.concatenate([p["istate"] for p in parts]), full.istate.cpu().numpy())
+    # the whole state, every field, in env order (the shards' slot layouts differ from the unsharded one's
+    # under the trigger-class layouts)
+    from ouzelum_amd import _lib as L
+    np.testing.assert_array_equal(np.concatenate([p["fstate"] for p in parts], axis=1),
+                                  full.frows(0, L.F_COUNT).cpu().numpy())
+    np.testing.assert_array_equal(np.concatenate([p["istate"] for p in parts], axis=1),
+                                  full.irows(0, L.I_COUNT).cpu().numpy())
     np.testing.assert_array_equal(np.concatenate([p["obs"] for p in parts], axis=1), storage[0].cpu().numpy())
     np.testing.assert_array_equal(np.concatenate([p["rew"] for p in parts], axis=1), storage[1].cpu().numpy())
     assert rows[:, 1].sum() > 0, "no episode finished: the statistics comparison tested nothing"

@@ -29,7 +29,7 @@ def ouz():
 def make_pair(ouz, task, n, seed=0, **kw):
     env = ouz.make(seed=seed, task=task, num_envs=n, sim_device="cuda:0", rl_device="cuda:0", **kw)
     ocfg = Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=seed,
-                       **{k: v for k, v in kw.items() if k in ("convergence_time",)})
+                       **{k: v for k, v in kw.items() if k in ("convergence_time", "env_id_offset", "num_envs_total")})
     return env, Q.OracleEnv(ocfg)
 
 
@@ -59,10 +59,17 @@ def assert_close(name, a, b, atol, rtol):
         raise AssertionError(f"{name}: max violation at {idx}: gpu={a[idx]!r} oracle={b[idx]!r}")
 
 
-@pytest.mark.parametrize("task", TASKS)
-def test_single_step_parity(ouz, task):
+# QuadMixed assigns tasks to 1344-id chunks: shards straddling the LeeLanded | QuadTracking and the
+# QuadTracking | QuadFault chunk boundaries
+PARITY_CASES = [(t, 0) for t in TASKS if t != "QuadMixed"] + [("QuadMixed", 1244), ("QuadMixed", 2588)]
+
+
+@pytest.mark.parametrize("task,off", PARITY_CASES)
+def test_single_step_parity(ouz, task, off):
     n = 320
     kw = {"convergence_time": 25} if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else {}
+    if off:
+        kw.update(env_id_offset=off, num_envs_total=off + n + 1000)
     env, o = make_pair(ouz, task, n, seed=11, **kw)
     rs = np.random.RandomState(5)
     for k in range(60):
@@ -183,9 +190,10 @@ def test_deterministic_rerun(ouz, task):
 def test_shard_invariance(ouz, task):
     """Envs sharded over 2 'ranks' (env_id_offset) reproduce the unsharded run bit for bit:
     every draw and the shared PV trigger index are keyed on the global env id.
-    456 = 2 x 228: both shards end in a partial 64-env tile."""
+    456 = 2 x 228: both shards end in a partial 64-env tile (QuadMixed: 2 x 1500, shards across the
+    curriculum's chunk boundaries at 1344 and 2688)."""
     from ouzelum_amd import _lib as L
-    n = 456
+    n = 3000 if task == "QuadMixed" else 456
     full = ouz.make(seed=7, task=task, num_envs=n, sim_device="cuda:0", convergence_time=10)
     halves = [ouz.make(seed=7, task=task, num_envs=n // 2, sim_device="cuda:0", env_id_offset=r * n // 2,
                        num_envs_total=n, convergence_time=10) for r in range(2)]
@@ -571,6 +579,8 @@ def test_ragged_sizes_parity(ouz, task, n):
     """Single env, sub-wave, one-over-a-wave and one-over-the-64-env-block-limit sizes (the 256-lane
     block path, a 1-lane last wave): state, obs, reward and done masks match the oracle step by step."""
     kw = {"convergence_time": 3} if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else {}
+    if task == "QuadMixed":   # across a chunk boundary
+        kw.update(env_id_offset=1300, num_envs_total=4096)
     env, o = make_pair(ouz, task, n, seed=21, **kw)
     rs = np.random.RandomState(8)
     for k in range(8):
@@ -594,7 +604,8 @@ def test_c_host_example_runs():
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     exe = os.path.join(root, "examples", "c_host_step")
-    if not os.path.exists(exe):
+    hdr = os.path.join(root, "include", "ouzelum.h")
+    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(hdr):   # stale against the ABI
         from ouzelum_amd import build
         build.build_examples(verbose=False)
     out = subprocess.run([exe, "4096", "300"], capture_output=True, text=True, timeout=120)
