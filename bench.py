@@ -257,9 +257,13 @@ class Runner:
         self.rollouts(steps, fused)
         e1.record()
         torch.cuda.synchronize(dev)
+        # The clock stops at this rank's synchronize, and the job time is the MAX over ranks.  The region
+        # already ends in a collective that completes only once every rank has finished its steps (the
+        # rollouts' return statistics, ReturnAllReduce.finish), and the closing barrier that brackets the
+        # region follows the clock instead of adding its own latency to it.
+        el = time.perf_counter() - t0
         if world > 1:
             dist.barrier()
-        el = time.perf_counter() - t0
         # after the clock stops: the process's first hipEventElapsedTime costs ~10 us of host time
         gpu_us = e0.elapsed_time(e1) * 1e3 / steps
         if world > 1:
