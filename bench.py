@@ -71,6 +71,9 @@ BYTES_PER_ENV_STEP = {
     # + DR scales (12 r), platform xy + heading (12 r/w), trajectory type / index / scale (12 r, 4 w)
     "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 24 + 12 + 4,
 }
+# VecTask.step above 65 536 envs runs quad_step_pipe_kernel for these tasks
+PIPE_TASKS = ("Ouzelum", "QuadFault", "Landing")
+LATENCY_REGIME_ENVS = 65536
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0
 EPISODE_TRACK_BYTES = 8           # ep_ret r/w when track_episodes is on
@@ -186,7 +189,8 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
-            "kernel": "quad_rollout_kernel" if kernel == "rollout" else "quad_step_kernel",
+            "kernel": "quad_rollout_kernel" if kernel == "rollout" else (
+                "quad_step_pipe_kernel" if task in PIPE_TASKS and n > LATENCY_REGIME_ENVS else "quad_step_kernel"),
             "steps_per_launch": steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
             "bytes_per_launch": round(b * n * steps_per_launch), "kernel_us": round(us_per_step, 3),
             "kernel_us_per_launch": round(us_per_step * steps_per_launch, 3)}

@@ -20,8 +20,10 @@ def avg_counter(path_glob, counter, kernel="quad_step_kernel<"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
-                # the single-step launch (quad_step_kernel<TASK>), not quad_rollout_kernel<TASK>
-                if kernel in name and row.get("Counter_Name") == counter:
+                # the single-step launch (quad_step_kernel<TASK>, or its large-N pipelined form
+                # quad_step_pipe_kernel<TASK>), not quad_rollout_kernel<TASK>
+                hit = kernel in name or (kernel == "quad_step_kernel<" and "quad_step_pipe_kernel<" in name)
+                if hit and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 

@@ -16,7 +16,8 @@ def main():
                        recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if kname in row.get("Kernel_Name", ""):
+                name = row.get("Kernel_Name", "")
+                if kname in name or (mode != "rollout" and "quad_step_pipe_kernel<" in name):
                     vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     res = {"task": task, "num_envs": int(n), "mode": mode, "kernel": kname.rstrip("<"),
            "steps_per_launch": 16 if mode == "rollout" else 1}
