@@ -538,6 +538,27 @@ def test_large_n_matches_shards(ouz, task):
     assert torch.equal(full.obs_buf, torch.cat([h.obs_buf for h in halves], 0))
 
 
+def test_large_n_misaligned_mixed_shard(ouz):
+    """Above 65 536 envs the mixed curriculum keeps slot i = env i; a shard whose offset is not a multiple of
+    64 has waves straddling two 1344-id task chunks, which run each task's lanes in turn and store their
+    outputs per lane.  Such a shard (offset 100) reproduces the same global ids of an aligned env bit for bit."""
+    from ouzelum_amd import _lib as L
+    off, n = 100, 70000
+    full = ouz.make(seed=14, task="QuadMixed", num_envs=off + n, sim_device="cuda:0", convergence_time=5)
+    shard = ouz.make(seed=14, task="QuadMixed", num_envs=n, sim_device="cuda:0", env_id_offset=off,
+                     num_envs_total=off + n, convergence_time=5)
+    g = torch.Generator(device="cuda").manual_seed(6)
+    for _ in range(12):
+        a = torch.rand((off + n, 4), device="cuda", generator=g) * 2 - 1
+        full.step(a)
+        shard.step(a[off:].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(shard.frows(0, L.F_COUNT), full.frows(0, L.F_COUNT)[:, off:])
+    assert torch.equal(shard.irows(0, L.I_COUNT), full.irows(0, L.I_COUNT)[:, off:])
+    for b in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+        assert torch.equal(getattr(shard, b), getattr(full, b)[off:]), b
+
+
 @pytest.mark.parametrize("task", ["QuadFault", "Ouzelum", "Landing"])
 def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
     """Above 65 536 envs the RL tasks' VecTask.step runs quad_step_pipe_kernel (4 tiles per wave, the next
