@@ -16,6 +16,7 @@ import bench as B  # noqa: E402
 tasks = (sys.argv[1] if len(sys.argv) > 1 else "QuadFault,LeeLanded,Ouzelum").split(",")
 sizes = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "4194304").split(",")]
 tiles = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1,2,4,8").split(",")]
+KNOB = os.environ.get("AB_KNOB", "OUZ_PIPE_TILES")   # the creation-time knob varied (OUZ_MIXED_SPLIT: 0 / 1)
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 
@@ -23,7 +24,7 @@ for task in tasks:
     for n in sizes:
         ref = None
         for tpw in tiles:
-            os.environ["OUZ_PIPE_TILES"] = str(tpw)
+            os.environ[KNOB] = str(tpw)
             env = B.make_env(task, n, dev, 1234, 0, n)
             ring = B.action_ring(n, dev, 1234, depth=2)
             env.rollout(ring, 40)
@@ -43,7 +44,7 @@ for task in tasks:
             torch.cuda.synchronize(dev)
             us = s.elapsed_time(e) * 1e3 / reps
             r = B.roofline_entry("step", task, n, us) if task in B.BYTES_PER_ENV_STEP else {"frac": None}
-            print(json.dumps({"task": task, "num_envs": n, "tiles_per_wave": tpw, "us": round(us, 2),
+            print(json.dumps({"task": task, "num_envs": n, KNOB: tpw, "us": round(us, 2),
                               "frac": r["frac"], "bitwise_equal_to_1": same}), flush=True)
             del env, ring, sd
             torch.cuda.empty_cache()
