@@ -196,6 +196,39 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
             "kernel_us_per_launch": round(us_per_step * steps_per_launch, 3)}
 
 
+class HipEvents:
+    """Two timing events recorded with hipEventRecord through ctypes on torch's own HIP runtime, on the step
+    stream.  torch.cuda.Event.record() costs ~5 us of host time against ~1.5 us for the raw call
+    (scripts/exp/event_record_cost.py), and the start event's host time is inside the timed region."""
+
+    def __init__(self, dev):
+        import ctypes
+        self._ct = ctypes
+        self.hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        self.ev = [ctypes.c_void_p(), ctypes.c_void_p()]
+        for e in self.ev:
+            if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
+                raise RuntimeError("hipEventCreate failed")
+        from ouzelum_amd import _lib
+        self.stream = ctypes.c_void_p(_lib.stream_ptr(dev))
+
+    def record(self, k):
+        if self.hip.hipEventRecord(self.ev[k], self.stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def __del__(self):
+        for e in getattr(self, "ev", []):
+            if e:
+                self.hip.hipEventDestroy(e)
+
+    def elapsed_ms(self):
+        ms = self._ct.c_float()
+        self.hip.hipEventSynchronize(self.ev[1])
+        if self.hip.hipEventElapsedTime(self._ct.byref(ms), self.ev[0], self.ev[1]) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+
 class Runner:
     """One env driven by 16-step rollouts: fused (``ouz_rollout_stats``, the headline) or one launch per step
     (``ouz_step_n_stats``, the VecTask.step path).  Statistics go to ``red``'s slots."""
@@ -247,19 +280,18 @@ class Runner:
         dev = self.dev
         if fused:
             self.prepare(steps)
-        # torch creates an event's HIP object lazily at its first record(); the first hipEventCreate of the
-        # process costs ~85 us of host time, which inside a 20-step region (~55 us of GPU work) would be
-        # most of the measured time.  Record both once before the region; the region re-records them.
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        e1.record()
+        # The events are created (the process's first hipEventCreate costs ~85 us of host time) and recorded
+        # once before the region; the region re-records them (raw hipEventRecord: HipEvents).
+        ev = HipEvents(dev)
+        ev.record(0)
+        ev.record(1)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
-        e0.record()
+        ev.record(0)
         self.rollouts(steps, fused)
-        e1.record()
+        ev.record(1)
         torch.cuda.synchronize(dev)
         # The clock stops at this rank's synchronize, and the job time is the MAX over ranks.  The region
         # already ends in a collective that completes only once every rank has finished its steps (the
@@ -269,7 +301,7 @@ class Runner:
         if world > 1:
             dist.barrier()
         # after the clock stops: the process's first hipEventElapsedTime costs ~10 us of host time
-        gpu_us = e0.elapsed_time(e1) * 1e3 / steps
+        gpu_us = ev.elapsed_ms() * 1e3 / steps
         if world > 1:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
