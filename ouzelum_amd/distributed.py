@@ -72,6 +72,7 @@ class ReturnAllReduce:
         self.filled = [0] * depth   # rows of the block submitted by the caller
         self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self._base = None
+        self._row_bytes = width * self.slots.element_size()
 
     def _where(self, r):
         return (r // self.batch) % self.depth, r % self.batch
@@ -97,6 +98,10 @@ class ReturnAllReduce:
 
     def slot_ptr(self, r):
         """Device address of ``slot(r)`` (the same waiting), for C entry points that take a double*."""
+        if not self.active:   # one rank: no collectives to wait for (the call sits before a timed launch)
+            if self._base is None:
+                self._base = self.slots.data_ptr()
+            return self._base + ((r // self.batch) % self.depth * self.batch + r % self.batch) * self._row_bytes
         d, row = self._where(r)
         if row == 0:
             self._wait(d)
@@ -106,12 +111,16 @@ class ReturnAllReduce:
         return self._base + (d * self.batch + row) * self.slots.shape[2] * 8
 
     def submit(self, r):
+        if not self.active:
+            return
         d, row = self._where(r)
         self.filled[d] = max(self.filled[d], row + 1)
         if row == self.batch - 1:
             self._flush(d, self.batch)
 
     def finish(self):
+        if not self.active:
+            return
         for d in range(self.depth):
             self._flush(d, self.filled[d])
             self._wait(d)
