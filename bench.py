@@ -201,10 +201,16 @@ class HipEvents:
     stream.  torch.cuda.Event.record() costs ~5 us of host time against ~1.5 us for the raw call
     (scripts/exp/event_record_cost.py), and the start event's host time is inside the timed region."""
 
+    LIB = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+
+    @classmethod
+    def available(cls):
+        return os.path.exists(cls.LIB)
+
     def __init__(self, dev):
         import ctypes
         self._ct = ctypes
-        self.hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        self.hip = ctypes.CDLL(self.LIB)
         self.ev = [ctypes.c_void_p(), ctypes.c_void_p()]
         for e in self.ev:
             if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
@@ -227,6 +233,19 @@ class HipEvents:
         if self.hip.hipEventElapsedTime(self._ct.byref(ms), self.ev[0], self.ev[1]) != 0:
             raise RuntimeError("hipEventElapsedTime failed")
         return ms.value
+
+
+class TorchEvents:
+    """HipEvents' interface over torch.cuda.Event (fallback)."""
+
+    def __init__(self):
+        self.ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
+
+    def record(self, k):
+        self.ev[k].record()
+
+    def elapsed_ms(self):
+        return self.ev[0].elapsed_time(self.ev[1])
 
 
 class Runner:
@@ -281,8 +300,9 @@ class Runner:
         if fused:
             self.prepare(steps)
         # The events are created (the process's first hipEventCreate costs ~85 us of host time) and recorded
-        # once before the region; the region re-records them (raw hipEventRecord: HipEvents).
-        ev = HipEvents(dev)
+        # once before the region; the region re-records them (raw hipEventRecord: HipEvents; torch's
+        # events if torch's HIP runtime library cannot be opened).
+        ev = HipEvents(dev) if HipEvents.available() else TorchEvents()
         ev.record(0)
         ev.record(1)
         torch.cuda.synchronize(dev)
