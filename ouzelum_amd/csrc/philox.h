@@ -63,7 +63,11 @@ OUZ_HD float unit_f32(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f
 OUZ_HD float uniform_f32(uint32_t x, float lo, float hi) {
 #pragma clang fp contract(off)   // two roundings, never an FMA (the oracle's numpy order)
 #if defined(__HIP_DEVICE_COMPILE__)
-  return lo + (hi - lo) * unit_f32(x);
+  // (hi - lo) * unit_f32(x) with the 2^-24 scale moved onto the span: both scalings by a power of two are
+  // exact (spans are normal floats), so the one rounding of the product is the same -- one multiply less
+  // per draw (QuadFault draws 13 noise factors per env-step)
+  const float span_s = (hi - lo) * (1.0f / 16777216.0f);
+  return lo + span_s * (float)(x >> 8);
 #else
   volatile float span = hi - lo;
   volatile float m = span * unit_f32(x);
