@@ -71,8 +71,9 @@ BYTES_PER_ENV_STEP = {
     # + DR scales (12 r), platform xy + heading (12 r/w), trajectory type / index / scale (12 r, 4 w)
     "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 24 + 12 + 4,
 }
-# VecTask.step above 65 536 envs runs quad_step_pipe_kernel for these tasks
+# VecTask.step above 2 M envs runs quad_step_pipe_kernel for these tasks (kPipeMinEnvs)
 PIPE_TASKS = ("Ouzelum", "QuadFault", "Landing")
+PIPE_MIN_ENVS = 2097152
 LATENCY_REGIME_ENVS = 65536
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0
@@ -180,20 +181,50 @@ def load_traffic(kernel, task, n):
             "source": os.path.relpath(hits[-1], ROOT)}
 
 
+def streamed_rollout(task, n):
+    """ouz_rollout of the tasks without the estimator above 131 072 envs: one step launch per step into the
+    storage rows (stream_rollout_default in quad_kernels.hip)."""
+    return n > 2 * LATENCY_REGIME_ENVS and task not in ("EKFLeeLanded", "QuadTracking", "QuadMixed")
+
+
+def streamed_rollout_bytes_per_env_step(task, k=RING):
+    """Algorithmic bytes per env-step of a streamed K-step rollout: the step kernel's (its outputs go to the
+    storage row, its flags come from the previous row), plus per rollout the last row copied from the env
+    buffers (65 B r + w) and the statistics launch's episode accumulators (12 B r)."""
+    return BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES + (2 * _STEP_OUT + 12) / k
+
+
+def step_kernel_name(task, n):
+    return "quad_step_pipe_kernel" if task in PIPE_TASKS and n > PIPE_MIN_ENVS else "quad_step_kernel"
+
+
 def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
-    """``us_per_step``: GPU time per env-step batch; a launch covers ``steps_per_launch`` steps."""
-    b = (rollout_bytes_per_env_step(task, steps_per_launch) if kernel == "rollout"
-         else BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES)
+    """``us_per_step``: GPU time per env-step batch; a launch covers ``steps_per_launch`` steps.  A streamed
+    rollout is priced as what it runs: ``steps_per_launch`` step launches, with their bytes."""
+    streamed = kernel == "rollout" and streamed_rollout(task, n)
+    if streamed:
+        b = streamed_rollout_bytes_per_env_step(task, steps_per_launch)
+    elif kernel == "rollout":
+        b = rollout_bytes_per_env_step(task, steps_per_launch)
+    else:
+        b = BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES
     achieved = b * n / (us_per_step * 1e-6) / 1e9
-    traffic = load_traffic(kernel, task, n)
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5),
-            "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
-            "kernel": "quad_rollout_kernel" if kernel == "rollout" else (
-                "quad_step_pipe_kernel" if task in PIPE_TASKS and n > LATENCY_REGIME_ENVS else "quad_step_kernel"),
-            "steps_per_launch": steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
-            "bytes_per_launch": round(b * n * steps_per_launch), "kernel_us": round(us_per_step, 3),
-            "kernel_us_per_launch": round(us_per_step * steps_per_launch, 3)}
+    # a streamed rollout's launches are step kernels writing a storage row instead of the env buffers (the same
+    # bytes): priced with the step kernel's PMC summary
+    traffic = load_traffic("step" if streamed else kernel, task, n)
+    e = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBPS, 5),
+         "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
+         "kernel": "quad_rollout_kernel" if kernel == "rollout" and not streamed else step_kernel_name(task, n),
+         "steps_per_launch": 1 if streamed else steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
+         "bytes_per_launch": round(b * n * (1 if streamed else steps_per_launch)), "kernel_us": round(us_per_step, 3),
+         "kernel_us_per_launch": round(us_per_step * (1 if streamed else steps_per_launch), 3)}
+    if streamed:
+        e["rollout"] = (f"streamed: {steps_per_launch} step launches per {steps_per_launch}-step rollout, straight "
+                        "into the storage rows, then the statistics launch (the per-rollout copy and statistics "
+                        "bytes are spread over the steps)")
+        e["steps_per_rollout"] = steps_per_launch
+    return e
 
 
 class HipEvents:
@@ -380,7 +411,8 @@ def sweep_entries(task, sizes, dev, seed):
         e.record()
         torch.cuda.synchronize(dev)
         out.append(roofline_entry("step", task, big, s.elapsed_time(e) * 1e3 / reps))
-        # the fused rollout at the same size: 16 steps per launch into (16, N, ...) storage + fused statistics
+        # ouz_rollout_stats at the same size (16 steps into (16, N, ...) storage + statistics): above the
+        # latency regime it streams the steps (one step launch each) instead of the fused kernel
         st = (torch.empty((RING, big, 13), device=dev), torch.empty((RING, big), device=dev),
               torch.empty((RING, big), dtype=torch.int64, device=dev),
               torch.empty((RING, big), dtype=torch.bool, device=dev))

@@ -25,7 +25,11 @@
  *                   registers, per-step obs/rew/reset/time_outs go to rollout storage [K][N][...]
  *                   (the learners' obs[step] = next_obs buffers, PPO/main.py:67-73,88-96) or to the
  *                   env buffers.  For the Lee tasks actions are ignored (ekf_lee_landed.py:308), so a
- *                   fused rollout is exactly K VecTask.step calls.
+ *                   fused rollout is exactly K VecTask.step calls.  Above 65 536 envs (or with
+ *                   OUZ_ROLLOUT_STREAM=1 at ouz_create; =0 keeps the fused launches) the rollout is
+ *                   streamed instead: one step launch per step writing straight into the storage rows,
+ *                   the statistics from a separate launch; bitwise K ouz_step calls (the fused
+ *                   launches agree with those within float tolerance: other code generation).
  *   ouz_pre_physics the task's pre_physics_step alone (ekf_lee_landed.py:308-530, lee_landed.py:263-330,
  *                   ouzelum.py:218-251): lazy reset, estimator / controller / guidance / thrust model, and the
  *                   body wrench handed to apply_rigid_body_force_tensors; no integration, no outputs, the
@@ -239,7 +243,8 @@ int ouz_rollout(ouz_env* env, const float* action_ring, int32_t ring_len, int32_
                 float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, void* stream);
 /* ouz_rollout followed by the rollout's episode statistics (as ouz_episode_stats would write them),
  * reduced inside the last rollout launch: one launch per rollout of <= 32 steps, no statistics kernel
- * (RPO-LSTM/main.py:96-110: T env steps, then RecordEpisodeStatisticsTorch's returns). */
+ * (RPO-LSTM/main.py:96-110: T env steps, then RecordEpisodeStatisticsTorch's returns).  A streamed
+ * rollout (see ouz_rollout) writes them with ouz_episode_stats after its last step. */
 int ouz_rollout_stats(ouz_env* env, const float* action_ring, int32_t ring_len, int32_t n_steps, float* obs_out,
                       float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int32_t drain,
                       void* stream);

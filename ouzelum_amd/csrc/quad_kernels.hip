@@ -33,6 +33,11 @@ constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS stagin
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
 constexpr int kLatencyRegimeEnvs = 65536;
 constexpr int kPipeTilesPerWave = 4;   // quad_step_pipe_kernel (large-N VecTask.step)
+// ... used above this many envs: where the RL tasks' state (~250 MB at 2 M envs) outgrows the 256 MB MALL
+// and each state load pays the HBM latency; below it the one-tile kernel is faster (fewer waves in flight
+// per tile: 131 072 envs 8.3 against 19.6 us, 2 M 104 against 120 us; 4 M 215-262 against 191-241 us,
+// profiles/r02/pipe_step_kernel_sizes_ab.jsonl)
+constexpr int kPipeMinEnvs = 2097152;
 // s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt / lgkmcnt left at their maxima (no wait)
 constexpr int kWaitVmcnt0 = (0x7 << 4) | (0xF << 8);
 
@@ -166,6 +171,10 @@ struct StepArgs {
   float* rew;
   int64_t* reset;
   uint8_t* timeouts;
+  // reset_buf / time_outs as the step reads them (the previous step's flags): the env buffers, or the
+  // previous storage row of a streamed rollout (ouz_rollout above the latency regime)
+  const int64_t* rst_in;
+  const uint8_t* to_in;
   const float2* wp_tab;        // lemniscate[100] | circle[100] | square[4]
   int32_t n;
   int32_t n_slots;             // state slots: n, or the trigger-class layout's padded count
@@ -423,10 +432,11 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   // loads and the state loads below are in flight together (one memory round trip, not three:
   // a short-circuit `!rst && timeouts == 0` made the time-out load wait for the reset load).
   // i: env index (the class layout's env-order buffers are not lane-contiguous)
-  const int64_t rv = CLS ? a.reset[i] : (a.reset + S.T.first)[S.T.l];
-  const uint32_t tv = CLS ? a.timeouts[i] : (a.timeouts + S.T.first)[S.T.l];
+  const int64_t rv = CLS ? a.rst_in[i] : (a.rst_in + S.T.first)[S.T.l];
+  const uint32_t tv = CLS ? a.to_in[i] : (a.to_in + S.T.first)[S.T.l];
   S.rst = rv != 0;
-  S.flags_clear = (rv == 0) & (tv == 0u);
+  // flags read from another buffer than the outputs (streamed rollout): the outputs are always written
+  S.flags_clear = (rv == 0) & (tv == 0u) & (a.rst_in == a.reset);
   S.p = ld3(S.T, OUZ_F_P);
   S.q = Q4{ld(S.T, OUZ_F_Q), ld(S.T, OUZ_F_Q + 1), ld(S.T, OUZ_F_Q + 2), ld(S.T, OUZ_F_Q + 3)};
   S.v = ld3(S.T, OUZ_F_V);
@@ -1328,6 +1338,16 @@ __host__ __device__ constexpr bool pipe_task(int task) {
   return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_LANDING;
 }
 
+// Streamed ouz_rollout by default (see ouz_env::stream_rollout): the tasks without the estimator above
+// 131 072 envs.  The estimator tasks keep the fused kernel at every size: their state (~600 B per env-step
+// of step-kernel traffic) is what the register-resident rollout saves, and it stays faster
+// (QuadTracking 4 M: 404 fused against 663 us per step streamed; LeeLanded 4 M: 262 against 147;
+// profiles/r02/stream_rollout_ab.jsonl).
+__host__ __device__ constexpr bool stream_rollout_default(int task, int n) {
+  return n > 2 * kLatencyRegimeEnvs && task != OUZ_TASK_EKF_LEE_LANDED && task != OUZ_TASK_TRACKING &&
+         task != OUZ_TASK_MIXED;
+}
+
 template <int TASK>
 __global__ void __launch_bounds__(kMaxBlock) OUZ_PIPE_ATTR quad_step_pipe_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
@@ -1657,6 +1677,11 @@ struct ouz_env {
   double* wave_partials;     // [tiles][3] per-wave partials of the fused rollout statistics
   uint32_t* wave_ticket;     // their last-wave counter (returns to 0 after every launch)
   StepArgs args;    // pre-filled launch arguments
+  // ouz_rollout as one step launch per step, outputs straight into the storage rows (streamed rollout):
+  // above the latency regime the fused kernel's 16 steps of state in registers cost occupancy (LeeLanded
+  // 177 VGPRs, 2 waves per SIMD, against the step kernel's 5) and it runs ~2x slower per step than the
+  // step kernel.  OUZ_ROLLOUT_STREAM=0/1 overrides.
+  bool stream_rollout;
   // Whole-batch flicker coins of steps [mask_lo, mask_lo + kMaskCache): a pure function of (seed, task,
   // step), drawn on the host (6 Philox blocks per step for a flickering task, ~0.3 us).  Filled for the
   // next launch's steps right after a launch is submitted, while the GPU runs it, so a launch does not
@@ -1793,7 +1818,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   if (pipe_task(cfg->task) && cfg->num_envs > kLatencyRegimeEnvs) {
     // tiles per wave of quad_step_pipe_kernel (OUZ_PIPE_TILES overrides; <= 1: the one-tile-per-wave kernel)
     const char* pt = std::getenv("OUZ_PIPE_TILES");
-    const int per_wave = pt ? std::atoi(pt) : kPipeTilesPerWave;
+    const int per_wave = pt ? std::atoi(pt) : (cfg->num_envs > kPipeMinEnvs ? kPipeTilesPerWave : 1);
     if (per_wave > 1) {
       const int tiles = (cfg->num_envs + 63) / 64, wpb = kMaxBlock / 64;
       const int waves = (tiles + per_wave - 1) / per_wave;
@@ -1801,6 +1826,10 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     }
   }
   a.trace_env = -1;
+  {
+    const char* rs = std::getenv("OUZ_ROLLOUT_STREAM");
+    e->stream_rollout = rs ? std::atoi(rs) != 0 : stream_rollout_default(cfg->task, cfg->num_envs);
+  }
   // x500 lumped mass properties (assets/x500/x500.urdf:31-35,98-177)
   const double base_m = 2.0, rm = 0.016076923076923075;
   const double mass = base_m + 4 * rm;
@@ -1857,6 +1886,8 @@ int ouz_bind(ouz_env* env, const ouz_buffers* b) {
   a.rew = b->rew;
   a.reset = b->reset;
   a.timeouts = b->timeouts;
+  a.rst_in = b->reset;
+  a.to_in = b->timeouts;
   return OUZ_OK;
 }
 
@@ -1939,8 +1970,9 @@ static void prefill_flicker_masks(ouz_env* env, int64_t from, int count) {
 // ring: action batches [ring_len][N][4] (step k uses batch (ring_pos + k) % ring_len) or null.
 // storage: per-step outputs for these K steps ([K][N][...]) or null (outputs go to the env buffers).
 static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64_t ring_pos, int32_t K,
-                        const OutPtrs* storage, hipStream_t s, double* stats_out = nullptr, int stats_mode = 0) {
-  const StepArgs& a = env->args;
+                        const OutPtrs* storage, hipStream_t s, double* stats_out = nullptr, int stats_mode = 0,
+                        const StepArgs* args = nullptr) {
+  const StepArgs& a = args ? *args : env->args;
   const int n = env->cfg.num_envs, blk = block_for(n);
   RolloutArgs r;
   std::memset(&r, 0, sizeof(r));
@@ -2012,6 +2044,41 @@ static int rollout_impl(ouz_env* env, const float* ring, int32_t ring_len, int32
   if (store && !(obs_out && rew_out && reset_out && timeouts_out))
     return fail(OUZ_ERR_INVALID, std::string(fn) + ": give all four storage pointers or none");
   const size_t n = (size_t)env->cfg.num_envs;
+  if (env->stream_rollout) {
+    // Streamed: step k reads the flags of row k - 1 and writes row k; the last step writes the env buffers,
+    // which are then copied into the last row.  Bitwise K VecTask.step calls (the fused kernel is the same
+    // per-env code in another loop, equal within float tolerance: tests/test_gpu_env.py).
+    const hipStream_t s = (hipStream_t)stream;
+    for (int32_t k = 0; k < n_steps; ++k) {
+      StepArgs a = env->args;
+      if (store && k > 0) {
+        a.rst_in = reset_out + (size_t)(k - 1) * n;
+        a.to_in = timeouts_out + (size_t)(k - 1) * n;
+      }
+      if (store && k + 1 < n_steps) {
+        a.obs = obs_out + (size_t)k * n * OUZ_NUM_OBS;
+        a.rew = rew_out + (size_t)k * n;
+        a.reset = reset_out + (size_t)k * n;
+        a.timeouts = timeouts_out + (size_t)k * n;
+      }
+      rc = launch_steps(env, ring, ring_len, k, 1, nullptr, s, nullptr, 0, &a);
+      if (rc) return rc;
+    }
+    if (store && n_steps > 0) {
+      const size_t last = (size_t)(n_steps - 1) * n;
+      const ouz_buffers& b = env->buf;
+      rc = hip_check(hipMemcpyAsync(obs_out + last * OUZ_NUM_OBS, b.obs, n * OUZ_NUM_OBS * sizeof(float),
+                                    hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(rollout obs)");
+      if (!rc) rc = hip_check(hipMemcpyAsync(rew_out + last, b.rew, n * sizeof(float), hipMemcpyDeviceToDevice, s),
+                              "hipMemcpyAsync(rollout rew)");
+      if (!rc) rc = hip_check(hipMemcpyAsync(reset_out + last, b.reset, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s),
+                              "hipMemcpyAsync(rollout reset)");
+      if (!rc) rc = hip_check(hipMemcpyAsync(timeouts_out + last, b.timeouts, n, hipMemcpyDeviceToDevice, s),
+                              "hipMemcpyAsync(rollout timeouts)");
+      if (rc) return rc;
+    }
+    return stats_mode ? ouz_episode_stats(env, stats_out, stats_mode == 2 ? 1 : 0, stream) : OUZ_OK;
+  }
   for (int32_t k0 = 0; k0 < n_steps; k0 += kMaxRolloutChunk) {
     const int32_t K = (n_steps - k0) < kMaxRolloutChunk ? (n_steps - k0) : kMaxRolloutChunk;
     OutPtrs st{obs_out + (size_t)k0 * n * OUZ_NUM_OBS, rew_out + (size_t)k0 * n, reset_out + (size_t)k0 * n,

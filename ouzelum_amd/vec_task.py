@@ -383,7 +383,9 @@ class QuadVecTask:
         ``(T, N, 4)`` (``None`` for the Lee tasks, which ignore actions) with one C call.
 
         ``fused=False``: one kernel launch per step (``ouz_step_n``).  ``fused=True``: up to 32
-        steps per launch with the env state held in registers (``ouz_rollout``); with
+        steps per launch with the env state held in registers (``ouz_rollout``; above 65 536 envs, where
+        that kernel's register footprint costs more than the state traffic it saves, one step launch per
+        step instead, bitwise K single steps); with
         ``storage=(obs (K,N,13), rew (K,N), reset (K,N) int64, time_outs (K,N) bool)`` every
         step's outputs land in the learner's rollout buffers, the env buffers keep the last step.
         ``stats_out`` (a float64 device tensor of >= 3): also write the episode statistics after

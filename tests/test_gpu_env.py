@@ -561,9 +561,9 @@ def test_large_n_misaligned_mixed_shard(ouz):
 
 @pytest.mark.parametrize("task", ["QuadFault", "Ouzelum", "Landing"])
 def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
-    """Above 65 536 envs the RL tasks' VecTask.step runs quad_step_pipe_kernel (4 tiles per wave, the next
-    tile's state loads in flight during this tile's compute); OUZ_PIPE_TILES=1 at env creation selects the
-    one-tile-per-wave quad_step_kernel.  Ragged size (a 37-lane last wave, a partial last stride) and a
+    """Above 2 M envs the RL tasks' VecTask.step runs quad_step_pipe_kernel (4 tiles per wave, the next
+    tile's state loads in flight during this tile's compute); OUZ_PIPE_TILES at env creation selects it with
+    that many tiles per wave from 65 537 envs on (1: the one-tile-per-wave quad_step_kernel).  Ragged size (a 37-lane last wave, a partial last stride) and a
     sharded twin: state and outputs bit for bit equal over 30 steps with resets."""
     from ouzelum_amd import _lib as L
     n = 70016 + 37
@@ -592,6 +592,58 @@ def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
             assert torch.equal(getattr(envs[k], b), getattr(ref, b)), (k, b)
     assert torch.equal(shard.frows(0, L.F_COUNT), ref.frows(0, L.F_COUNT)[:, 66000:])
     assert torch.equal(shard.obs_buf, ref.obs_buf[66000:])
+
+
+@pytest.mark.parametrize("task,n,off", [("LeeLanded", 70016 + 37, 0), ("QuadFault", 70016 + 37, 0),
+                                        ("QuadTracking", 3000, 0), ("QuadMixed", 4096, 1300),
+                                        ("Ouzelum", 1000, 0)])
+def test_streamed_rollout_matches_single_steps(ouz, task, n, off, monkeypatch):
+    """Above 65 536 envs ouz_rollout / ouz_rollout_stats run one step launch per step with the outputs written
+    straight into the storage rows (the next step reads its reset / time-out flags from the previous row);
+    OUZ_ROLLOUT_STREAM=1 at env creation forces that path at any size.  It is VecTask.step K times: storage
+    rows == the env buffers after each single step, state and statistics bit for bit, over a 16-step, a
+    40-step and a 1-step rollout with drained and kept statistics.  (The fused kernel is the same per-env
+    code compiled into another loop: within float tolerance of the single steps,
+    test_fused_rollout_matches_single_steps.)  Covers the pipelined step kernel (QuadFault), the
+    trigger-class layout (QuadTracking) and a misaligned mixed shard."""
+    from ouzelum_amd import _lib as L
+    kw = dict(seed=17, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True,
+              env_id_offset=off, num_envs_total=off + n)
+    if task in ("QuadTracking", "QuadMixed"):
+        kw["convergence_time"] = 10
+    if task in ("LeeLanded", "QuadTracking"):
+        kw["max_episode_length"] = 30
+    monkeypatch.setenv("OUZ_ROLLOUT_STREAM", "1")
+    a = ouz.make(**kw)
+    monkeypatch.setenv("OUZ_ROLLOUT_STREAM", "0")
+    b = ouz.make(**kw)
+    monkeypatch.delenv("OUZ_ROLLOUT_STREAM")
+    g = torch.Generator(device="cuda").manual_seed(12)
+    ring = (torch.rand((16, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
+    total = 0.0
+    for k_steps, drain in ((16, True), (40, False), (1, True), (16, True)):
+        st = (torch.full((k_steps, n, 13), -7.0, device="cuda"), torch.full((k_steps, n), -7.0, device="cuda"),
+              torch.full((k_steps, n), -7, dtype=torch.int64, device="cuda"),
+              torch.ones((k_steps, n), dtype=torch.bool, device="cuda"))
+        got = torch.full((3,), -1.0, dtype=torch.float64, device="cuda")
+        a.rollout(ring, k_steps, fused=True, storage=st, stats_out=got, drain=drain)
+        rows = ([], [], [], [])
+        for k in range(k_steps):
+            b.step(ring[k % 16])
+            for r, buf in zip(rows, (b.obs_buf, b.rew_buf, b.reset_buf, b.timeout_buf)):
+                r.append(buf.clone())
+        want = b.episode_stats(drain=drain).clone()
+        torch.cuda.synchronize()
+        for name, x, r in zip(("obs", "rew", "reset", "time_outs"), st, rows):
+            assert torch.equal(x, torch.stack(r)), (k_steps, name)
+        assert torch.equal(a.frows(0, L.F_COUNT), b.frows(0, L.F_COUNT))
+        assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT))
+        for buf in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+            assert torch.equal(getattr(a, buf), getattr(b, buf)), buf
+        assert torch.equal(got, want)
+        assert a.sim_step_count == b.sim_step_count
+        total += float(got[1])
+    assert total > 0, "no episode finished: the test would not test anything"
 
 
 @pytest.mark.parametrize("task,n", [("LeeLanded", 1), ("EKFLeeLanded", 63), ("QuadFault", 65), ("QuadTracking", 130),
