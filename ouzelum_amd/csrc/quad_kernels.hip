@@ -184,6 +184,7 @@ struct StepArgs {
   uint64_t seed;
   int32_t track_episodes;
   int32_t pipe_stride;         // quad_step_pipe_kernel: waves in its grid (0: that kernel is not used)
+  int32_t nt_loads;            // step kernels: non-temporal state loads (large N: nt_loads_default)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
@@ -356,6 +357,9 @@ __device__ __forceinline__ Tile tile_of(const StepArgs& a, int i) {
   return Tile{ftile(a, i), itile(a, i), (uint32_t)i & 63u, wave_tile(i) * 64u};
 }
 __device__ __forceinline__ float ld(const Tile& t, int field) { return t.f[(uint32_t)field * 64u + t.l]; }
+__device__ __forceinline__ float ld_nt(const Tile& t, int field) {
+  return __builtin_nontemporal_load(&t.f[(uint32_t)field * 64u + t.l]);
+}
 // State and staged-output stores are non-temporal (`global_store ... nt`): nothing in the step reads
 // them back, and at large N they are a write stream of 118-700 B per env-step.  Measured against
 // plain stores: 4 M envs LeeLanded HBM fraction 0.59 -> 0.76, QuadFault 0.47 -> 0.54,
@@ -368,6 +372,9 @@ __device__ __forceinline__ float ld(const Tile& t, int field) { return t.f[(uint
 #endif
 __device__ __forceinline__ void st(const Tile& t, int field, float v) { OUZ_ST(&t.f[(uint32_t)field * 64u + t.l], v); }
 __device__ __forceinline__ int32_t ldi(const Tile& t, int field) { return t.iv[(uint32_t)field * 64u + t.l]; }
+__device__ __forceinline__ int32_t ldi_nt(const Tile& t, int field) {
+  return __builtin_nontemporal_load(&t.iv[(uint32_t)field * 64u + t.l]);
+}
 __device__ __forceinline__ void sti(const Tile& t, int field, int32_t v) { OUZ_ST(&t.iv[(uint32_t)field * 64u + t.l], v); }
 __device__ __forceinline__ V3 ld3(const Tile& t, int f) { return v3(ld(t, f), ld(t, f + 1), ld(t, f + 2)); }
 __device__ __forceinline__ void st3(const Tile& t, int f, V3 v) { st(t, f, v.x); st(t, f + 1, v.y); st(t, f + 2, v.z); }
@@ -425,7 +432,7 @@ __device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL,
   }
 }
 
-template <int CTRL, int TGT, bool CLS = false>
+template <int CTRL, int TGT, bool CLS = false, bool NTL = false>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S,
                                          const float* actions) {
   // reset_buf and time_outs are read unconditionally and combined without a branch, so the two flag
@@ -437,49 +444,53 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   S.rst = rv != 0;
   // flags read from another buffer than the outputs (streamed rollout): the outputs are always written
   S.flags_clear = (rv == 0) & (tv == 0u) & (a.rst_in == a.reset);
-  S.p = ld3(S.T, OUZ_F_P);
-  S.q = Q4{ld(S.T, OUZ_F_Q), ld(S.T, OUZ_F_Q + 1), ld(S.T, OUZ_F_Q + 2), ld(S.T, OUZ_F_Q + 3)};
-  S.v = ld3(S.T, OUZ_F_V);
-  S.w = ld3(S.T, OUZ_F_W);
-  S.progress = ldi(S.T, OUZ_I_PROGRESS);
+  // NTL: non-temporal state loads (large N: see nt_loads_default)
+  const auto L = [&](int f) -> float { return NTL ? ld_nt(S.T, f) : ld(S.T, f); };
+  const auto LI = [&](int f) -> int32_t { return NTL ? ldi_nt(S.T, f) : ldi(S.T, f); };
+  const auto L3 = [&](int f) -> V3 { return v3(L(f), L(f + 1), L(f + 2)); };
+  S.p = L3(OUZ_F_P);
+  S.q = Q4{L(OUZ_F_Q), L(OUZ_F_Q + 1), L(OUZ_F_Q + 2), L(OUZ_F_Q + 3)};
+  S.v = L3(OUZ_F_V);
+  S.w = L3(OUZ_F_W);
+  S.progress = LI(OUZ_I_PROGRESS);
   S.dirty = 0;
   // The landing flag is only needed on reset.  In the latency regime (few waves per CU: the step is
   // one dependent chain, load -> compute -> store) it is fetched with the state so the reset branch,
   // taken by most waves once episodes desynchronise, does not wait on a second memory round trip.
   // At large N that 4-byte load would be bandwidth; there the reset branch fetches it on demand.
-  S.land_flag = a.n <= kLatencyRegimeEnvs ? ldi(S.T, OUZ_I_LAND_FLAG) : -1;
+  S.land_flag = a.n <= kLatencyRegimeEnvs ? LI(OUZ_I_LAND_FLAG) : -1;
   S.landings_add = 0;
   S.ep_cnt_add = 0;
   S.ep_len_add = 0;
   S.ep_sum_add = 0.0f;
-  S.ep_ret = a.track_episodes ? ld(S.T, OUZ_F_EP_RET) : 0.0f;
+  S.ep_ret = a.track_episodes ? L(OUZ_F_EP_RET) : 0.0f;
   S.dr_m = S.dr_i = S.dr_t = 1.0f;
-  if (tp.dr) { S.dr_m = ld(S.T, OUZ_F_DR); S.dr_i = ld(S.T, OUZ_F_DR + 1); S.dr_t = ld(S.T, OUZ_F_DR + 2); }
-  if constexpr (TGT == TGT_GOAL) S.target = ld3(S.T, OUZ_F_TARGET);
+  if (tp.dr) { S.dr_m = L(OUZ_F_DR); S.dr_i = L(OUZ_F_DR + 1); S.dr_t = L(OUZ_F_DR + 2); }
+  if constexpr (TGT == TGT_GOAL) S.target = L3(OUZ_F_TARGET);
   if constexpr (CTRL == CTRL_RL) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) S.thrust[k] = ld(S.T, OUZ_F_THRUST + k);
+    for (int k = 0; k < 4; ++k) S.thrust[k] = L(OUZ_F_THRUST + k);
     S.frot = -1; S.fonset = 0; S.eta = 1.0f;
-    if (tp.fault) { S.frot = ldi(S.T, OUZ_I_FAULT_ROTOR); S.fonset = ldi(S.T, OUZ_I_FAULT_ONSET); S.eta = ld(S.T, OUZ_F_FAULT_ETA); }
+    if (tp.fault) { S.frot = LI(OUZ_I_FAULT_ROTOR); S.fonset = LI(OUZ_I_FAULT_ONSET); S.eta = L(OUZ_F_FAULT_ETA); }
     // in flight with the state loads: issued inside the step it would be a second memory round trip
     // behind the reset branch (every wave's critical path, and half the bytes in flight at large N)
     load_actions<CTRL, TGT, CLS>(actions, S, i);
   }
   if constexpr (CTRL == CTRL_LEE_EST) {
-    S.prev_v = ld3(S.T, OUZ_F_PREV_V);
-    S.wp = ld3(S.T, OUZ_F_WAYPOINT);
-    S.eq = EkfQ{ld(S.T, OUZ_F_EKF_Q), ld(S.T, OUZ_F_EKF_Q + 1), ld(S.T, OUZ_F_EKF_Q + 2), ld(S.T, OUZ_F_EKF_Q + 3)};
+    S.prev_v = L3(OUZ_F_PREV_V);
+    S.wp = L3(OUZ_F_WAYPOINT);
+    S.eq = EkfQ{L(OUZ_F_EKF_Q), L(OUZ_F_EKF_Q + 1), L(OUZ_F_EKF_Q + 2), L(OUZ_F_EKF_Q + 3)};
 #pragma unroll
-    for (int k = 0; k < 10; ++k) S.eP[k] = ld(S.T, OUZ_F_EKF_P + k);
+    for (int k = 0; k < 10; ++k) S.eP[k] = L(OUZ_F_EKF_P + k);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) S.px[k] = ld(S.T, OUZ_F_PV_X + k);
+    for (int k = 0; k < 9; ++k) S.px[k] = L(OUZ_F_PV_X + k);
 #pragma unroll
-    for (int k = 0; k < 45; ++k) S.pP[k] = ld(S.T, OUZ_F_PV_P + k);
+    for (int k = 0; k < 45; ++k) S.pP[k] = L(OUZ_F_PV_P + k);
   }
   if constexpr (TGT == TGT_TRAJ) {
-    S.plat = make_float2(ld(S.T, OUZ_F_PLAT), ld(S.T, OUZ_F_PLAT + 1));
-    S.ttype = ldi(S.T, OUZ_I_TRAJ_TYPE); S.tidx = ldi(S.T, OUZ_I_TRAJ_IDX);
-    S.tsd = ld(S.T, OUZ_F_TRAJ_SD); S.heading = ld(S.T, OUZ_F_PLAT_HEADING);
+    S.plat = make_float2(L(OUZ_F_PLAT), L(OUZ_F_PLAT + 1));
+    S.ttype = LI(OUZ_I_TRAJ_TYPE); S.tidx = LI(OUZ_I_TRAJ_IDX);
+    S.tsd = L(OUZ_F_TRAJ_SD); S.heading = L(OUZ_F_PLAT_HEADING);
 
   } else {
     S.plat = make_float2(0.0f, 0.0f);
@@ -987,7 +998,7 @@ struct LaneStats {
 
 // i: state slot (its wave tile is wave-uniform); e: env index (== i except under the trigger-class layout,
 // CLS), which keys the RNG and indexes the env-order buffers.
-template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false>
+template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
                                         bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
@@ -998,7 +1009,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT, CLS>(a, e, tp, S, ctx[0].actions);
+  if (valid) env_load<CTRL, TGT, CLS, NTL>(a, e, tp, S, ctx[0].actions);
   // fused statistics: the episode accumulators of earlier (unfused) steps, in flight with the state
   float ep_sum_old = 0.0f;
   int32_t ep_cnt_old = 0, ep_len_old = 0;
@@ -1184,7 +1195,7 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, int n, int 
   }
 }
 
-template <int TASK, bool MULTI, bool PRE = false, bool CLS = false>
+template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
@@ -1204,15 +1215,15 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
   if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
-    run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
-    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED) {
-    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE, CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_EST, TGT_PLATFORM, MULTI, PRE, CLS, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LANDING) {
-    run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
-    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+    run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (CLS) {
     // mixed curriculum, class layout: a wave's slots lie in one 1344-id chunk, so its task is wave-uniform
     const uint32_t c = a.env_offset / kClassBlock + __builtin_amdgcn_readfirstlane((uint32_t)first) / kClassBlock;
@@ -1235,13 +1246,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     const bool vl = valid && t == OUZ_TASK_LEE_LANDED, vt = valid && t == OUZ_TASK_TRACKING;
     const bool vr = valid && !vl && !vt;
     if (__any(vl))
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vl,
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vl,
                                                   OUZ_TASK_LEE_LANDED, direct, sm, &ls, wrench);
     if (__any(vt))
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vt,
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vt,
                                              OUZ_TASK_TRACKING, direct, sm, &ls, wrench);
     if (__any(vr))
-      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
+      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
                                         direct, sm, &ls, wrench);
   }
   if (sm) reduce_stats(*rst, CLS ? a.n_slots : a.n, first, ls);
@@ -1250,11 +1261,11 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
 // (~390 B): the host copies the argument block on every launch (≈0.6 us more host time per launch
 // for a 1.1 KB block, scripts/exp/launch_cost.hip), and at 4096 envs that host time is the bound.
-template <int TASK, bool CLS = false>
+template <int TASK, bool CLS = false, bool NTL = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false, false, CLS>(a, &c, 1, env_out, 0);
+  step_body<TASK, false, false, CLS, NTL>(a, &c, 1, env_out, 0);
 }
 
 // ouz_pre_physics: pre_physics_step alone, the body wrench to `wrench` [n][6].
@@ -1280,7 +1291,7 @@ __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, Rol
 // 80 registers more: a second copy would cost the occupancy this buys).
 constexpr size_t kCtxArgOffset = (sizeof(StepArgs) + alignof(StepCtx) - 1) / alignof(StepCtx) * alignof(StepCtx);
 
-template <int CTRL, int TGT>
+template <int CTRL, int TGT, bool NTL>
 __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, const OutPtrs& o, float* wave_lds,
                                           int t, int tiles, int task) {
   const TaskParams& tp = a.tp[tp_slot(task)];
@@ -1289,7 +1300,7 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
   bool valid = i < a.n;
   EnvRegs<CTRL, TGT> S;
   S.T = tile_of(a, i);
-  if (valid) env_load<CTRL, TGT>(a, i, tp, S, c.actions);
+  if (valid) env_load<CTRL, TGT, false, NTL>(a, i, tp, S, c.actions);
   for (;;) {
     // The argument blocks are re-read through laundered pointers every tile: otherwise the compiler
     // hoists the wave-uniform float arithmetic on them (VALU results, held in VGPRs) out of the loop,
@@ -1308,7 +1319,7 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
     EnvRegs<CTRL, TGT> N;
     N.T = tile_of(A, in);
 #ifndef OUZ_PIPE_NOPREF
-    if (vn) env_load<CTRL, TGT>(A, in, TP, N, C.actions);
+    if (vn) env_load<CTRL, TGT, false, NTL>(A, in, TP, N, C.actions);
 #endif
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
@@ -1321,7 +1332,7 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
     if (valid) env_store<CTRL, TGT>(A, i, TP, S);
     if (!more) break;
 #ifdef OUZ_PIPE_NOPREF
-    if (vn) env_load<CTRL, TGT>(A, in, TP, N, C.actions);
+    if (vn) env_load<CTRL, TGT, false, NTL>(A, in, TP, N, C.actions);
 #endif
     S = N;
     t = tn;
@@ -1338,6 +1349,16 @@ __host__ __device__ constexpr bool pipe_task(int task) {
   return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_LANDING;
 }
 
+// Non-temporal state loads in the step kernels above 2 M envs (LeeLanded: 4 M).  Below, part of the state
+// is still MALL-resident from the previous step and plain loads keep it there; above, the loads only evict
+// what the write stream needs.  Measured crossovers (profiles/r02/nt_loads_ab.txt, per-step kernel us
+// plain -> non-temporal): QuadTracking 2 M 281 -> 301, 4 M 663 -> 581 / 671 -> 626; QuadMixed 1 M 97 -> 99,
+// 2 M 196 -> 188, 4 M 376 -> 355; QuadFault 4 M 227 -> 223 / 239 -> 224; LeeLanded 4 M 124 -> 128 /
+// 126 -> 140, 8 M 267 -> 244, 16 M 605 -> 566.
+__host__ __device__ constexpr bool nt_loads_default(int task, int n) {
+  return n > (task == OUZ_TASK_LEE_LANDED ? 4194304 : 2097152);
+}
+
 // Streamed ouz_rollout by default (see ouz_env::stream_rollout): the tasks without the estimator above
 // 131 072 envs.  The estimator tasks keep the fused kernel at every size: their state (~600 B per env-step
 // of step-kernel traffic) is what the register-resident rollout saves, and it stays faster
@@ -1348,7 +1369,7 @@ __host__ __device__ constexpr bool stream_rollout_default(int task, int n) {
          task != OUZ_TASK_MIXED;
 }
 
-template <int TASK>
+template <int TASK, bool NTL = false>
 __global__ void __launch_bounds__(kMaxBlock) OUZ_PIPE_ATTR quad_step_pipe_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
   __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
@@ -1357,8 +1378,8 @@ __global__ void __launch_bounds__(kMaxBlock) OUZ_PIPE_ATTR quad_step_pipe_kernel
   const int t = (int)__builtin_amdgcn_readfirstlane(blockIdx.x * (kMaxBlock / 64) + (threadIdx.x >> 6));
   const int tiles = (a.n + 63) >> 6;
   if (t >= tiles) return;
-  if constexpr (TASK == OUZ_TASK_LANDING) pipe_envs<CTRL_RL, TGT_TRAJ>(a, c, o, wave_lds, t, tiles, TASK);
-  else if constexpr (pipe_task(TASK)) pipe_envs<CTRL_RL, TGT_GOAL>(a, c, o, wave_lds, t, tiles, TASK);
+  if constexpr (TASK == OUZ_TASK_LANDING) pipe_envs<CTRL_RL, TGT_TRAJ, NTL>(a, c, o, wave_lds, t, tiles, TASK);
+  else if constexpr (pipe_task(TASK)) pipe_envs<CTRL_RL, TGT_GOAL, NTL>(a, c, o, wave_lds, t, tiles, TASK);
 }
 
 // Creation-time state (VecTask.allocate_buffers vec_task.py:254-277 + task __init__).
@@ -1827,6 +1848,11 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   }
   a.trace_env = -1;
   {
+    const char* nl = std::getenv("OUZ_NT_LOADS");
+    a.nt_loads = (nl ? std::atoi(nl) != 0 : nt_loads_default(cfg->task, cfg->num_envs)) ? 1 : 0;
+    if (a.cls) a.nt_loads = 0;   // the trigger-class layout (<= 64 K envs) has no such instantiation
+  }
+  {
     const char* rs = std::getenv("OUZ_ROLLOUT_STREAM");
     e->stream_rollout = rs ? std::atoi(rs) != 0 : stream_rollout_default(cfg->task, cfg->num_envs);
   }
@@ -1925,8 +1951,9 @@ extern "C++" template <int T>
 static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, dim3 g, dim3 b, hipStream_t s) {
   if constexpr (pipe_task(T)) {
     if (single && a.pipe_stride) {
-      hipLaunchKernelGGL((quad_step_pipe_kernel<T>), dim3(a.pipe_stride / (kMaxBlock / 64)), dim3(kMaxBlock), 0, s,
-                         a, r.ctx[0]);
+      const dim3 pg(a.pipe_stride / (kMaxBlock / 64)), pb(kMaxBlock);
+      if (a.nt_loads) hipLaunchKernelGGL((quad_step_pipe_kernel<T, true>), pg, pb, 0, s, a, r.ctx[0]);
+      else hipLaunchKernelGGL((quad_step_pipe_kernel<T, false>), pg, pb, 0, s, a, r.ctx[0]);
       return;
     }
   }
@@ -1937,7 +1964,8 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
       return;
     }
   }
-  if (single) hipLaunchKernelGGL((quad_step_kernel<T, false>), g, b, 0, s, a, r.ctx[0]);
+  if (single && a.nt_loads) hipLaunchKernelGGL((quad_step_kernel<T, false, true>), g, b, 0, s, a, r.ctx[0]);
+  else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false>), g, b, 0, s, a, r.ctx[0]);
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 

@@ -1,15 +1,12 @@
 #!/bin/bash
-# A/B of alternative in-tree builds of the library (OUZ_LIB) on the bench's 2000-step line with configs and sweep.
-set -u
-for lib in ${LIBS:-libouzelum_hip}; do
-  OUZ_LIB=$PWD/ouzelum_amd/$lib.so timeout -k 10 300 python -u bench.py --steps 2000 --warmup 100 --no-cpu-baseline ${SWEEP:---no-sweep} > gpurun_out/ab_$lib.json || exit 1
-  python - $lib <<PY
-import json, sys
-d = json.load(open(f"gpurun_out/ab_{sys.argv[1]}.json"))
-print(sys.argv[1], "B %.4g" % d["value"], d["roofline"]["kernel_us"], "per-step b2b", d["per_step_launch"]["roofline"]["kernel_us_back_to_back"],
-      " ".join(f"{s['kernel'][5:9]}{s['num_envs']}:{s['frac']:.3f}" for s in d.get("roofline_sweep", [])))
-for c in d.get("configs", []):
-    print("   ", c["config"], "%.4g" % c["value"], c["roofline"]["kernel_us"], "per-step b2b", c["per_step_launch"]["roofline"]["kernel_us_back_to_back"],
-          " ".join(f"{s['kernel'][5:9]}:{s['frac']:.3f}" for s in c.get("roofline_sweep", [])))
-PY
+# A/B of two in-tree library builds on the large-N step kernel: scripts/exp/pipe_ab.py under the product
+# library and under OUZ_LIB=$1, alternating twice.  Usage: bash scripts/exp/lib_ab.sh <variant.so> TASKS SIZES TILES
+set -eu
+cd "$(dirname "$0")/../.."
+V=$1; T=$2; S=$3; P=${4:-1}
+for r in 1 2; do
+  echo "# product build (round $r)"
+  timeout -k 10 300 python -u scripts/exp/pipe_ab.py "$T" "$S" "$P"
+  echo "# $V (round $r)"
+  OUZ_LIB=$PWD/$V timeout -k 10 300 python -u scripts/exp/pipe_ab.py "$T" "$S" "$P"
 done

@@ -594,6 +594,40 @@ def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
     assert torch.equal(shard.obs_buf, ref.obs_buf[66000:])
 
 
+@pytest.mark.parametrize("task,pipe", [("LeeLanded", None), ("QuadTracking", None), ("QuadMixed", None),
+                                       ("QuadFault", "4"), ("Landing", "1")])
+def test_nt_load_step_kernels_match(ouz, task, pipe, monkeypatch):
+    """Large-N step kernels with non-temporal state loads (default above 2 M envs, LeeLanded 4 M;
+    OUZ_NT_LOADS=0/1 at env creation forces them off / on from 65 537 envs): only the cache policy
+    differs, so state and outputs are bit for bit those of the plain-load kernels, 25 steps with resets,
+    ragged size, one-tile and pipelined kernels."""
+    from ouzelum_amd import _lib as L
+    n = 70016 + 37
+    if pipe:
+        monkeypatch.setenv("OUZ_PIPE_TILES", pipe)
+    envs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("OUZ_NT_LOADS", mode)
+        kw = {"convergence_time": 10} if task in ("QuadTracking", "QuadMixed") else {}
+        envs[mode] = ouz.make(seed=23, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True,
+                              max_episode_length=12, **kw)
+    monkeypatch.delenv("OUZ_NT_LOADS")
+    g = torch.Generator(device="cuda").manual_seed(6)
+    done = 0
+    for _ in range(25):
+        a = torch.rand((n, 4), device="cuda", generator=g) * 4 - 2
+        for e in envs.values():
+            e.step(a)
+        done += int(envs["0"].reset_buf.sum())
+    torch.cuda.synchronize()
+    assert done > 0
+    x, y = envs["0"], envs["1"]
+    assert torch.equal(x.frows(0, L.F_COUNT), y.frows(0, L.F_COUNT))
+    assert torch.equal(x.irows(0, L.I_COUNT), y.irows(0, L.I_COUNT))
+    for b in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+        assert torch.equal(getattr(x, b), getattr(y, b)), b
+
+
 @pytest.mark.parametrize("task,n,off", [("LeeLanded", 70016 + 37, 0), ("QuadFault", 70016 + 37, 0),
                                         ("QuadTracking", 3000, 0), ("QuadMixed", 4096, 1300),
                                         ("Ouzelum", 1000, 0)])
