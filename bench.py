@@ -71,9 +71,6 @@ BYTES_PER_ENV_STEP = {
     # + DR scales (12 r), platform xy + heading (12 r/w), trajectory type / index / scale (12 r, 4 w)
     "QuadTracking": _CORE + 2 * (12 + 56 + 216 + 12) + 12 + 24 + 12 + 4,
 }
-# VecTask.step above 2 M envs runs quad_step_pipe_kernel for these tasks (kPipeMinEnvs)
-PIPE_TASKS = ("Ouzelum", "QuadFault", "Landing")
-PIPE_MIN_ENVS = 2097152
 LATENCY_REGIME_ENVS = 65536
 BYTES_PER_ENV_STEP["QuadMixed"] = (BYTES_PER_ENV_STEP["LeeLanded"] + BYTES_PER_ENV_STEP["QuadTracking"]
                                    + BYTES_PER_ENV_STEP["QuadFault"]) / 3.0
@@ -195,7 +192,9 @@ def streamed_rollout_bytes_per_env_step(task, k=RING):
 
 
 def step_kernel_name(task, n):
-    return "quad_step_pipe_kernel" if task in PIPE_TASKS and n > PIPE_MIN_ENVS else "quad_step_kernel"
+    """The VecTask.step kernel at this size (quad_step_pipe_kernel is opt-in: OUZ_PIPE_TILES)."""
+    return "quad_step_pipe_kernel" if int(os.environ.get("OUZ_PIPE_TILES", "1")) > 1 and n > LATENCY_REGIME_ENVS \
+        and task in ("Ouzelum", "QuadFault", "Landing") else "quad_step_kernel"
 
 
 def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):

@@ -32,12 +32,12 @@ constexpr int kMaxBlock = 256;   // step/rollout kernel launch bound (LDS stagin
 // At or below this many envs a launch has at most 4 waves per CU and the step is latency-bound;
 // above it, bandwidth-bound (the launch grid switches from 64- to 256-lane blocks at the same size).
 constexpr int kLatencyRegimeEnvs = 65536;
-constexpr int kPipeTilesPerWave = 4;   // quad_step_pipe_kernel (large-N VecTask.step)
-// ... used above this many envs: where the RL tasks' state (~250 MB at 2 M envs) outgrows the 256 MB MALL
-// and each state load pays the HBM latency; below it the one-tile kernel is faster (fewer waves in flight
-// per tile: 131 072 envs 8.3 against 19.6 us, 2 M 104 against 120 us; 4 M 215-262 against 191-241 us,
-// profiles/r02/pipe_step_kernel_sizes_ab.jsonl)
-constexpr int kPipeMinEnvs = 2097152;
+// quad_step_pipe_kernel (the RL tasks' large-N VecTask.step with the next tile's state in flight): opt-in
+// through OUZ_PIPE_TILES=<tiles per wave> at env creation.  It beat the one-tile kernel only while the
+// state loads were plain (4 M envs QuadFault 215-241 against 245-262 us); with the non-temporal loads of
+// nt_loads_default the one-tile kernel is faster (QuadFault 4 M 190-200 against 210-223 us, 8 M 410-423
+// against 416-458; Ouzelum equal within 2 %: profiles/r02/pipe_step_kernel_sizes_ab.jsonl).
+constexpr int kPipeTilesDefault = 1;
 // s_waitcnt immediate (gfx9 encoding): vmcnt(0), expcnt / lgkmcnt left at their maxima (no wait)
 constexpr int kWaitVmcnt0 = (0x7 << 4) | (0xF << 8);
 
@@ -1837,9 +1837,9 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   a.track_episodes = cfg->track_episodes;
   a.pipe_stride = 0;
   if (pipe_task(cfg->task) && cfg->num_envs > kLatencyRegimeEnvs) {
-    // tiles per wave of quad_step_pipe_kernel (OUZ_PIPE_TILES overrides; <= 1: the one-tile-per-wave kernel)
+    // tiles per wave of quad_step_pipe_kernel (OUZ_PIPE_TILES; default and <= 1: the one-tile-per-wave kernel)
     const char* pt = std::getenv("OUZ_PIPE_TILES");
-    const int per_wave = pt ? std::atoi(pt) : (cfg->num_envs > kPipeMinEnvs ? kPipeTilesPerWave : 1);
+    const int per_wave = pt ? std::atoi(pt) : kPipeTilesDefault;
     if (per_wave > 1) {
       const int tiles = (cfg->num_envs + 63) / 64, wpb = kMaxBlock / 64;
       const int waves = (tiles + per_wave - 1) / per_wave;

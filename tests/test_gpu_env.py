@@ -561,9 +561,9 @@ def test_large_n_misaligned_mixed_shard(ouz):
 
 @pytest.mark.parametrize("task", ["QuadFault", "Ouzelum", "Landing"])
 def test_pipelined_step_kernel_matches_one_tile_kernel(ouz, task, monkeypatch):
-    """Above 2 M envs the RL tasks' VecTask.step runs quad_step_pipe_kernel (4 tiles per wave, the next
-    tile's state loads in flight during this tile's compute); OUZ_PIPE_TILES at env creation selects it with
-    that many tiles per wave from 65 537 envs on (1: the one-tile-per-wave quad_step_kernel).  Ragged size (a 37-lane last wave, a partial last stride) and a
+    """quad_step_pipe_kernel (the RL tasks' large-N VecTask.step with the next tile's state loads in flight
+    during this tile's compute; opt-in: OUZ_PIPE_TILES=<tiles per wave> at env creation, from 65 537 envs
+    on; 1, the default: the one-tile-per-wave quad_step_kernel).  Ragged size (a 37-lane last wave, a partial last stride) and a
     sharded twin: state and outputs bit for bit equal over 30 steps with resets."""
     from ouzelum_amd import _lib as L
     n = 70016 + 37
