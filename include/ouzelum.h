@@ -25,15 +25,19 @@
  *                   registers, per-step obs/rew/reset/time_outs go to rollout storage [K][N][...]
  *                   (the learners' obs[step] = next_obs buffers, PPO/main.py:67-73,88-96) or to the
  *                   env buffers.  For the Lee tasks actions are ignored (ekf_lee_landed.py:308), so a
- *                   fused rollout is exactly K VecTask.step calls.  Above 65 536 envs (or with
- *                   OUZ_ROLLOUT_STREAM=1 at ouz_create; =0 keeps the fused launches) the rollout is
- *                   streamed instead: one step launch per step writing straight into the storage rows,
- *                   the statistics from a separate launch; bitwise K ouz_step calls (the fused
- *                   launches agree with those within float tolerance: other code generation).
+ *                   fused rollout is exactly K VecTask.step calls.  Above 131 072 envs for the tasks
+ *                   without the estimator (not EKFLeeLanded / QuadTracking / QuadMixed), or with
+ *                   OUZ_ROLLOUT_STREAM=1 at ouz_create (=0 keeps the fused launches at every size), the
+ *                   rollout is streamed instead: one step launch per step writing straight into the
+ *                   storage rows, the statistics from a separate launch; bitwise K ouz_step calls.  The
+ *                   fused launches agree with those within float tolerance (other code generation), so
+ *                   results go from bitwise-equal-to-ouz_step to within-tolerance at that boundary.
  *   ouz_pre_physics the task's pre_physics_step alone (ekf_lee_landed.py:308-530, lee_landed.py:263-330,
  *                   ouzelum.py:218-251): lazy reset, estimator / controller / guidance / thrust model, and the
  *                   body wrench handed to apply_rigid_body_force_tensors; no integration, no outputs, the
- *                   step counter does not advance (a component entry for parity tests, not half a step)
+ *                   step counter does not advance (a component entry for parity tests, not half a step).
+ *                   It writes the pre-physics env state back (lazy reset, thrusts, EKF / PV filters,
+ *                   waypoint; reset_buf cleared): restore the state before stepping on with the same step
  *   ouz_reset_idx   VecTask.reset_idx / reset_done (lazy: marks reset_buf)
  *                                              tasks/base/vec_task.py:369-406, ekf_lee_landed.py:271-306
  *   ouz_lee_control Controller.__call__        controllers/controller.py:45-48 (+ position/velocity/attitude)
@@ -224,6 +228,12 @@ typedef struct ouz_task_info {
 typedef struct ouz_env ouz_env;
 
 int32_t ouz_abi_version(void);
+/* Instrumentation compiled into this library (0 for the product build): timing-stamp builds and
+ * store-policy A/B builds give the product's results but are not the product; the Python shim
+ * refuses them unless OUZ_ALLOW_INSTRUMENTED=1 (tests/test_abi.py checks the shipped library is 0). */
+#define OUZ_BUILD_STAMPS 1u
+#define OUZ_BUILD_TEMPORAL_STORES 2u
+uint32_t ouz_build_flags(void);
 /* State slots of a task at num_envs (see "State slots" above); negative on bad arguments. */
 int64_t ouz_state_slots(int32_t task, int32_t num_envs);
 /* State slot of each of num_envs envs of a shard starting at global id env_id_offset, into the host

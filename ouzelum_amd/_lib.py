@@ -37,6 +37,7 @@ F_EP_RET, F_EP_SUM, F_PLAT_HEADING = 101, 102, 103
 F_COUNT = 104
 I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT, I_EP_LEN = range(9)
 I_COUNT = 9
+BUILD_STAMPS, BUILD_TEMPORAL_STORES = 1, 2  # ouz_build_flags bits
 TILE = 64  # OUZ_TILE: state is [tiles][fields][64] (ouzelum.h OUZ_FIDX)
 
 
@@ -83,6 +84,7 @@ _I64 = ctypes.c_int64
 # name -> (restype, argtypes).  This table IS the list of symbols include/ouzelum.h declares.
 SIGNATURES = {
     "ouz_abi_version": (_I, []),
+    "ouz_build_flags": (_U32, []),
     "ouz_state_slots": (_I64, [_I, _I]),
     "ouz_env_slots": (_I, [_I, _I, _I64, _P]),
     "ouz_last_error": (ctypes.c_char_p, []),
@@ -135,6 +137,12 @@ def _load():
         fn.argtypes = args
     if lib.ouz_abi_version() != ABI_VERSION:
         raise OuzelumError(f"ABI mismatch: library {lib.ouz_abi_version()} != binding {ABI_VERSION}")
+    flags = lib.ouz_build_flags()
+    if flags and os.environ.get("OUZ_ALLOW_INSTRUMENTED") != "1":
+        raise OuzelumError(f"{LIB_PATH} is an instrumented build (ouz_build_flags = {flags:#x}: "
+                           f"{'stamps ' if flags & BUILD_STAMPS else ''}"
+                           f"{'temporal-stores' if flags & BUILD_TEMPORAL_STORES else ''}); "
+                           "set OUZ_ALLOW_INSTRUMENTED=1 to load it on purpose")
     return lib
 
 

@@ -96,9 +96,10 @@ __host__ inline int mixed_env_slot(uint32_t env_offset, int e) {   // its invers
   return (int)(c - env_offset / kClassBlock) * kClassBlock + rel;
 }
 
-// Probe build only (-DOUZ_PROBE_STAMPS): per-wave s_memtime stamps at the phase boundaries of the
-// single-step kernel, read back with ouz_probe_stamps.  Not part of the product library.
-#ifdef OUZ_PROBE_STAMPS
+// Instrumented build only (-DOUZ_STAMPS, scripts/build_probe.sh): per-wave s_memtime stamps at the phase
+// boundaries, read back with ouz_probe_stamps.  The results are those of the product build; the build reports
+// itself through ouz_build_flags() and the Python shim refuses to load it unless OUZ_ALLOW_INSTRUMENTED=1.
+#ifdef OUZ_STAMPS
 constexpr int kStampSlots = 32, kStampWaves = 1024;   // 0-12 step phases, 13-29 rollout step starts, 30-31 mid-rollout step
 __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
 #define OUZ_STAMP(k, wait)                                                                       \
@@ -364,7 +365,7 @@ __device__ __forceinline__ float ld_nt(const Tile& t, int field) {
 // them back, and at large N they are a write stream of 118-700 B per env-step.  Measured against
 // plain stores: 4 M envs LeeLanded HBM fraction 0.59 -> 0.76, QuadFault 0.47 -> 0.54,
 // QuadMixed 0.53 -> 0.57, estimator tasks +-1 %, the 4096-env step unchanged (3.51 us).
-// -DOUZ_TEMPORAL_STORES restores plain stores for comparison.
+// -DOUZ_TEMPORAL_STORES restores plain stores for comparison (an A/B build: ouz_build_flags reports it).
 #ifdef OUZ_TEMPORAL_STORES
 #define OUZ_ST(p, v) (*(p) = (v))
 #else
@@ -682,11 +683,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     V3 tau;
     const V3 cmd = v3(0.0f, 0.0f, 1.0f);
     R0 = quat_to_mat(S.q);
-#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 1)
-    T = 0.5f + 0.01f * S.p.z; tau = S.w;
-#else
     lee_position_R(R0, S.p, S.v, S.w, cmd, 0.0f, default_gains(), T, tau);
-#endif
     float fz = 2.0f * kGravity * T;
     V3 dd = cmd - S.p;
     if (sqrtf(dot(dd, dd)) < tp.land_radius) {
@@ -732,11 +729,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       pomdp_apply<3>(vm, tp, task, a, sc, gid, SITE_VEL, false);
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
-#ifdef OUZ_PROBE_UNIFORM_TRIGGER   // probe only (wrong results): every lane takes its wave's first lane's triggers
-    const uint64_t g = (uint64_t)sc.step * a.n_total + __builtin_amdgcn_readfirstlane(gid);
-#else
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
-#endif
     {
       // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
       // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
@@ -810,9 +803,6 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
     if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);
-#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 2)
-    S.p = S.p + 0.01f * S.v; S.v = S.v + inv_m * f_b; S.w = S.w + mul(tau_b, inv_I) + I;
-#else
     if constexpr (CTRL == CTRL_RL) R0 = quat_to_mat(S.q);
     const DeckContact deck{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y};
     const float h = c.dt / (float)c.substeps;
@@ -820,7 +810,6 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       integrate_thrust_body<2>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck);
     else
       integrate_thrust_body<0>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck, c.substeps);
-#endif
   }
 
   OUZ_STAMP(4, false);
@@ -844,11 +833,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
 #pragma unroll
   for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
   float dist;
-#if defined(OUZ_PROBE_SKIP) && (OUZ_PROBE_SKIP & 4)
-  rew = p.x; dist = p.y;
-#else
   rew = reward(p, target, q, w, dist);
-#endif
   const bool timeout_len = S.progress >= tp.max_ep - 1;
   const bool die = dist > 8.0f || p.z < tp.z_die;
   rs = timeout_len || die;
@@ -910,14 +895,7 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
                                      float rew, bool rs, bool to, bool direct, bool keep_flags = false) {
   const uint32_t lane = (uint32_t)i & 63u;
   const uint32_t first = wave_tile(i) * 64u;   // wave-uniform: output bases live in SGPRs
-#if defined(OUZ_PROBE_EMIT) && OUZ_PROBE_EMIT == 1   // probe: no output stores at all
-  return;
-#endif
-#if defined(OUZ_PROBE_EMIT) && OUZ_PROBE_EMIT == 2   // probe: per-lane row stores at every size
-  if (!direct) {
-#else
   if (n <= kLatencyRegimeEnvs && !direct) {
-#endif
     // Latency regime (a few waves per CU, the step is one dependent chain): each lane stores its own
     // 52-byte row as three 16-byte stores + one dword (rows are 4-byte aligned; gfx950 global stores
     // take dword alignment), skipping the LDS round trip and the wave barrier of the staged form.
@@ -1032,14 +1010,10 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
-#ifdef OUZ_PROBE_NOCORE
-    for (int k = 0; k < OUZ_NUM_OBS; ++k) ob[k] = S.p.x * k;
-#else
     const bool did_reset = valid && S.rst;
     const bool flags_clear = valid && S.flags_clear;
     if (valid) env_core<CTRL, TGT>(a, ctx[0], e, gid, task, S, ob, rew, rs, to);
     trace_count(a, ctx[0].step, did_reset, i, e);
-#endif
     OUZ_STAMP(5, false);
     if (CLS) emit_env(outs[1], e, valid, ob, rew, rs, to, flags_clear);
     else emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
@@ -1318,9 +1292,7 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
     const bool vn = more && in < A.n;
     EnvRegs<CTRL, TGT> N;
     N.T = tile_of(A, in);
-#ifndef OUZ_PIPE_NOPREF
     if (vn) env_load<CTRL, TGT, false, NTL>(A, in, TP, N, C.actions);
-#endif
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
@@ -1331,9 +1303,6 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
     emit(o, wave_lds, i, A.n, valid, ob, rew, rs, to, false, flags_clear);
     if (valid) env_store<CTRL, TGT>(A, i, TP, S);
     if (!more) break;
-#ifdef OUZ_PIPE_NOPREF
-    if (vn) env_load<CTRL, TGT, false, NTL>(A, in, TP, N, C.actions);
-#endif
     S = N;
     t = tn;
     i = in;
@@ -1342,9 +1311,7 @@ __device__ __forceinline__ void pipe_envs(const StepArgs& a, const StepCtx& c, c
 }
 
 // Three waves per SIMD: unconstrained the loop takes 170 VGPRs (two waves); at four the allocator spills.
-#ifndef OUZ_PIPE_ATTR
 #define OUZ_PIPE_ATTR __attribute__((amdgpu_waves_per_eu(3, 3)))
-#endif
 __host__ __device__ constexpr bool pipe_task(int task) {
   return task == OUZ_TASK_OUZELUM || task == OUZ_TASK_FAULT || task == OUZ_TASK_LANDING;
 }
@@ -1715,7 +1682,7 @@ struct ouz_env {
 
 extern "C" {
 
-#ifdef OUZ_PROBE_STAMPS
+#ifdef OUZ_STAMPS
 int ouz_probe_stamps(uint64_t* host, int32_t count) {
   const int n = count < kStampWaves * kStampSlots ? count : kStampWaves * kStampSlots;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ouz_stamps), (size_t)n * sizeof(uint64_t)) == hipSuccess ? n : -1;
@@ -1723,6 +1690,17 @@ int ouz_probe_stamps(uint64_t* host, int32_t count) {
 #endif
 
 int32_t ouz_abi_version(void) { return OUZ_ABI_VERSION; }
+
+uint32_t ouz_build_flags(void) {
+  uint32_t f = 0;
+#ifdef OUZ_STAMPS
+  f |= OUZ_BUILD_STAMPS;
+#endif
+#ifdef OUZ_TEMPORAL_STORES
+  f |= OUZ_BUILD_TEMPORAL_STORES;
+#endif
+  return f;
+}
 
 int64_t ouz_state_slots(int32_t task, int32_t num_envs) {
   if (task < 0 || task >= OUZ_NUM_TASKS || num_envs <= 0) return fail(OUZ_ERR_INVALID, "ouz_state_slots: bad task / size");

@@ -223,7 +223,10 @@ class QuadVecTask:
         """The task's pre_physics_step alone (``ouz_pre_physics``): lazy reset, estimator / controller /
         guidance / thrust model applied to the env state, and the (N, 6) body wrench (force, torque in the
         body frame) the reference hands to gym.apply_rigid_body_force_tensors.  The step counter does not
-        advance and nothing is integrated -- a component entry for parity tests, not half a step."""
+        advance and nothing is integrated -- a component entry for parity tests, not half a step.
+        It MODIFIES the env state: the lazy reset, thrust integrator, EKF / PV filters and waypoint are written
+        back and reset_buf is cleared for the envs it reset, so a following ``step`` with the same step counter
+        would run them again.  Save ``state_dict()`` before and load it after if the env is to step on."""
         wrench = torch.empty((self.num_envs, 6), dtype=torch.float32, device=self.device)
         L.check(L.lib.ouz_pre_physics(self._env, self._actions_ptr(actions), L.ptr(wrench), self._stream()),
                 "ouz_pre_physics")
@@ -383,9 +386,12 @@ class QuadVecTask:
         ``(T, N, 4)`` (``None`` for the Lee tasks, which ignore actions) with one C call.
 
         ``fused=False``: one kernel launch per step (``ouz_step_n``).  ``fused=True``: up to 32
-        steps per launch with the env state held in registers (``ouz_rollout``; above 65 536 envs, where
-        that kernel's register footprint costs more than the state traffic it saves, one step launch per
-        step instead, bitwise K single steps); with
+        steps per launch with the env state held in registers (``ouz_rollout``; above 131 072 envs, for the
+        tasks without the estimator -- not EKFLeeLanded / QuadTracking / QuadMixed --, where that kernel's
+        register footprint costs more than the state traffic it saves, one step launch per step instead;
+        ``OUZ_ROLLOUT_STREAM=0/1`` at creation overrides.  The streamed form is bitwise K single steps, the
+        fused one equal to them within float tolerance, so results change from bitwise to within-tolerance
+        at that size); with
         ``storage=(obs (K,N,13), rew (K,N), reset (K,N) int64, time_outs (K,N) bool)`` every
         step's outputs land in the learner's rollout buffers, the env buffers keep the last step.
         ``stats_out`` (a float64 device tensor of >= 3): also write the episode statistics after
@@ -441,7 +447,9 @@ class QuadVecTask:
         (``ouz_rollout_stats``: the K steps fused into one launch per 32 steps with the episode statistics
         reduced in the last one) and no per-call checks.  ``stats_out_ptr`` is the device address of a
         contiguous float64 tensor of >= 3 on this device (e.g. a ``ReturnAllReduce`` slot).  The caller keeps
-        ``action_ring`` and ``storage`` alive while the plan is used."""
+        ``action_ring`` and ``storage`` alive while the plan is used.  The plan launches on torch's current
+        stream of the env device at each call (not the one current when it was built), so it is ordered with
+        the caller's work on that stream."""
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
         n_steps = int(n_steps)
@@ -467,10 +475,10 @@ class QuadVecTask:
                 if tuple(tns.shape[:len(shape)]) != shape or tns.dtype != dt:
                     raise ValueError(f"storage {name} must be {shape} {dt}")
             ptrs = [L.ptr(t) for t in storage]
-        fn, env, stream, dr = L.lib.ouz_rollout_stats, self._env, self._stream(), 1 if drain else 0
+        fn, env, dr, sp, dev = L.lib.ouz_rollout_stats, self._env, 1 if drain else 0, L.stream_ptr, self._dev_index
 
         def run(stats_out_ptr):
-            rc = fn(env, ring_ptr, ring_len, n_steps, ptrs[0], ptrs[1], ptrs[2], ptrs[3], stats_out_ptr, dr, stream)
+            rc = fn(env, ring_ptr, ring_len, n_steps, ptrs[0], ptrs[1], ptrs[2], ptrs[3], stats_out_ptr, dr, sp(dev))
             if rc:
                 L.check(rc, "ouz_rollout_stats")
         return run
@@ -493,15 +501,25 @@ class QuadVecTask:
         return self.obs_dict, done
 
     # ----------------------------------------------------------- state I/O
+    def _layout(self):
+        """What fixes the slot order of fstate / istate: the ABI's layout rules, the slot count and the shard's
+        place among the global ids (the mixed curriculum's slot map depends on env_id_offset)."""
+        return {"abi": L.ABI_VERSION, "slots": int(self.fstate.shape[0]) * L.TILE,
+                "env_id_offset": int(self.cfg.env_id_offset), "num_envs_total": int(self.cfg.num_envs_total)}
+
     def state_dict(self):
-        """Env-state checkpoint (the reference never checkpoints env state)."""
+        """Env-state checkpoint (the reference never checkpoints env state).  The state is saved in
+        slot order together with its layout marker; ``load_state_dict`` refuses a checkpoint of another layout."""
         return {"fstate": self.fstate.clone(), "istate": self.istate.clone(), "obs": self.obs_buf.clone(),
                 "rew": self.rew_buf.clone(), "reset": self.reset_buf.clone(), "timeouts": self.timeout_buf.clone(),
-                "step": self.sim_step_count, "task": self.task, "num_envs": self.num_envs}
+                "step": self.sim_step_count, "task": self.task, "num_envs": self.num_envs, "layout": self._layout()}
 
     def load_state_dict(self, sd):
         if sd["task"] != self.task or sd["num_envs"] != self.num_envs:
             raise ValueError("checkpoint is for a different task / env count")
+        if sd.get("layout") != self._layout():
+            raise ValueError(f"checkpoint state layout {sd.get('layout')} != this env's {self._layout()} "
+                             "(slot order differs: ABI version, slot count or shard offset)")
         self.fstate.copy_(sd["fstate"])
         self.istate.copy_(sd["istate"])
         self.obs_buf.copy_(sd["obs"])

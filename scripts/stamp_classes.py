@@ -4,6 +4,8 @@ PV-filter trigger pattern, so the wave's PV-step duration (stamps 11 -> 12) sort
 only, velocity fix, position fix, both fixes.  Per class: the PV step and the whole wave (entry -> stores
 landed); per launch: which class the last wave to finish belongs to, and by how much it trails the median
 wave.  Per-wave phases in shader cycles (s_memtime); cross-wave times in ns (s_memrealtime)."""
+import os
+os.environ.setdefault("OUZ_ALLOW_INSTRUMENTED", "1")  # the stamp build reports OUZ_BUILD_STAMPS
 import ctypes
 import json
 import sys

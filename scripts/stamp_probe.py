@@ -1,8 +1,10 @@
 """Phase timeline of the single-step kernel from per-wave s_memtime stamps (probe build:
-OUZ_EXTRA_FLAGS=-DOUZ_PROBE_STAMPS).  Stamps: 0 entry, 1 state loads landed, 2 reset done,
+OUZ_EXTRA_FLAGS=-DOUZ_STAMPS).  Stamps: 0 entry, 1 state loads landed, 2 reset done,
 3 controller done, 4 integrator done, 5 env_core done, 6 obs emitted, 7 stores landed;
 8 / 9 s_memrealtime (100 MHz) at entry / exit; estimator tasks: 10 / 11 around the AHRS-EKF update,
 12 after the PV-filter step."""
+import os
+os.environ.setdefault("OUZ_ALLOW_INSTRUMENTED", "1")  # the stamp build reports OUZ_BUILD_STAMPS
 import ctypes
 import sys
 

@@ -1,10 +1,12 @@
 """Per-step timeline of the fused rollout kernel from per-wave s_memtime stamps (probe build with
--DOUZ_PROBE_STAMPS, loaded through OUZ_LIB).  Slots 13..29: start of rollout steps 0..16 (29 = after the
+-DOUZ_STAMPS, loaded through OUZ_LIB).  Slots 13..29: start of rollout steps 0..16 (29 = after the
 last step); 30 / 31: mid-rollout step (k = 8) after env_core / after its stores were issued; 2 / 3 / 4: the
 last step's reset-done / controller-done / physics-done.
 
     OUZ_LIB=ouzelum_amd/libouzelum_probe.so python scripts/stamp_rollout.py LeeLanded 4096
 """
+import os
+os.environ.setdefault("OUZ_ALLOW_INSTRUMENTED", "1")  # the stamp build reports OUZ_BUILD_STAMPS
 import ctypes
 import sys
 
@@ -45,9 +47,14 @@ print(f"  step median {np.median(steps):.0f}  p90 {np.percentile(steps, 90):.0f}
 print(f"  k=8: env_core {np.median(st[:, 30] - st[:, 21]):.0f}, emit {np.median(st[:, 31] - st[:, 30]):.0f}, "
       f"to next step {np.median(st[:, 22] - st[:, 31]):.0f}")
 last = st[:, 28]
-print(f"  last step: prelude+reset {np.median(st[:, 2] - last):.0f}, controller {np.median(st[:, 3] - st[:, 2]):.0f}, "
+# stamps 2-4 / 10-12 are written from env_core; a build where the compiler dropped them leaves zeros, which
+# would print as huge negative spans (round 2's committed file had such rows): report them as not recorded
+if not (st[:, 2:5] > 0).all():
+    print("  last step: phase stamps 2-4 not recorded by this build")
+else:
+  print(f"  last step: prelude+reset {np.median(st[:, 2] - last):.0f}, controller {np.median(st[:, 3] - st[:, 2]):.0f}, "
       f"physics {np.median(st[:, 4] - st[:, 3]):.0f}, post+emit {np.median(st[:, 29] - st[:, 4]):.0f}")
-if st[:, 12].any():
+if (st[:, 10:13] > 0).all() and (st[:, 2:5] > 0).all():
     print(f"  last step estimator: inputs->EKF {np.median(st[:, 10] - st[:, 2]):.0f}, EKF {np.median(st[:, 11] - st[:, 10]):.0f}, "
           f"PV {np.median(st[:, 12] - st[:, 11]):.0f}, guidance+Lee {np.median(st[:, 3] - st[:, 12]):.0f}")
 print(f"  prologue: state loads issued -> landed {np.median(st[:, 1] - st[:, 0]):.0f}, landed -> first step "

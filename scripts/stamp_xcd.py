@@ -3,6 +3,8 @@ OUZ_LIB=ouzelum_amd/libouzelum_probe.so) at entry / exit of run_env, grouped by 
 (blockIdx % 8; 64-thread blocks at <= 64 K envs: one stamp row per block, empty rows are unused blocks).  Three regimes: one VecTask.step
 launch after an idle GPU, the last of 12 queued back to back, and a 16-step fused rollout after an idle GPU.
 Times in ns relative to the launch's first wave entry, medians over 40 launches."""
+import os
+os.environ.setdefault("OUZ_ALLOW_INSTRUMENTED", "1")  # the stamp build reports OUZ_BUILD_STAMPS
 import ctypes
 import json
 import sys

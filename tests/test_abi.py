@@ -149,3 +149,15 @@ def test_state_slots_and_class_layout_map(L):
     assert L.lib.ouz_env_slots(L.TASK_MIXED, 4, -1, bad.ctypes.data) < 0
 
 
+
+def test_shipped_library_is_not_instrumented(L):
+    """The product library carries no instrumentation: ouz_build_flags() is 0, the
+    wrong-result probe paths of earlier rounds are gone from the kernel source, and the shim refuses an
+    instrumented build (a timing-stamp or store-policy A/B library) unless OUZ_ALLOW_INSTRUMENTED=1."""
+    assert L.lib.ouz_build_flags() == 0
+    src = open(os.path.join(ROOT, "ouzelum_amd", "csrc", "quad_kernels.hip")).read()
+    for gone in ("OUZ_PROBE_SKIP", "OUZ_PROBE_UNIFORM_TRIGGER", "OUZ_PROBE_EMIT", "OUZ_PROBE_NOCORE",
+                 "OUZ_PIPE_NOPREF"):
+        assert gone not in src, gone
+    shim = open(os.path.join(ROOT, "ouzelum_amd", "_lib.py")).read()
+    assert "OUZ_ALLOW_INSTRUMENTED" in shim and "ouz_build_flags" in shim

@@ -244,6 +244,19 @@ def test_state_dict_roundtrip(ouz):
     for _ in range(15):
         env.step(None)
     assert torch.equal(a, env.fstate)
+    # a checkpoint of another slot layout is refused: another shard offset of the mixed
+    # curriculum, a layout-less (round-1 style) checkpoint
+    bad = dict(sd)
+    bad.pop("layout")
+    with pytest.raises(ValueError):
+        env.load_state_dict(bad)
+    m0 = ouz.make(seed=1, task="QuadMixed", num_envs=1344, sim_device="cuda:0", env_id_offset=0,
+                  num_envs_total=4032)
+    m1 = ouz.make(seed=1, task="QuadMixed", num_envs=1344, sim_device="cuda:0", env_id_offset=1344,
+                  num_envs_total=4032)
+    with pytest.raises(ValueError):
+        m1.load_state_dict(m0.state_dict())
+    m0.load_state_dict(m0.state_dict())
 
 
 @pytest.mark.parametrize("task,n", [("LeeLanded", 4096), ("QuadTracking", 4096), ("QuadFault", 8192),

@@ -1,4 +1,6 @@
 """Learner kernels and the recurrent training loop on the GPU."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -6,6 +8,7 @@ import torch
 from oracle import learner_oracle as LO
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_gae_kernel_bit_exact(golden):
@@ -202,3 +205,25 @@ def test_graphed_policy_matches_eager(recurrent, monkeypatch):
             assert not torch.equal(action, prev)
         prev = action.clone()
     assert agent._graphed is not None and agent._graphed.graph is not None
+
+
+def test_graph_replay_policy_follows_the_runtime_not_torch_flag():
+    """torch.cuda.is_available() starts the HIP runtime but leaves torch.cuda.is_initialized()
+    False.  GRAPH_REPLAY_SAFE must then be False (the runtime read packet capture = on), and True when the
+    package is imported first or the knob is in the process's initial environment."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "DEBUG_CLR_GRAPH_PACKET_CAPTURE"}
+    probe = "import ouzelum_amd as o; print(int(o.GRAPH_REPLAY_SAFE), int(o._hip_started))"
+    cases = {
+        "avail_first": ("import torch; assert torch.cuda.is_available(); " + probe, env, "0 1"),
+        "pkg_first": ("import torch, ouzelum_amd as o; torch.cuda.is_available(); "
+                      "print(int(o.GRAPH_REPLAY_SAFE), int(o._hip_started))", env, "1 0"),
+        "knob_in_env": ("import torch; assert torch.cuda.is_available(); " + probe,
+                        {**env, "DEBUG_CLR_GRAPH_PACKET_CAPTURE": "0"}, "1 1"),
+    }
+    for name, (code, e, want) in cases.items():
+        out = subprocess.run([sys.executable, "-c", code], env=e, cwd=ROOT, capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 0, (name, out.stderr[-2000:])
+        assert out.stdout.strip().splitlines()[-1] == want, (name, out.stdout)
