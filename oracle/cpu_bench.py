@@ -118,14 +118,16 @@ def _worker(task, n_total, off, n_local, seed, warm, steps, barrier, q):
     q.put(time.perf_counter() - t0)
 
 
-def vectorised(task, n, seed=0, budget_s=3.0, cores=None):
-    """env-steps/s of the batched oracle over ``cores`` worker processes (default: all host cores)."""
+def vectorised(task, n, seed=0, budget_s=3.0, cores=None, env_id_offset=0, n_total=None):
+    """env-steps/s of the batched oracle over ``cores`` worker processes (default: all host cores).
+    ``env_id_offset`` / ``n_total``: a shard of a larger global env range (config E's per-GPU shard)."""
     cores = cores or host_cores()
-    shards = _shards(n, min(cores, n))
+    n_total = n_total or n
+    shards = [(env_id_offset + o_, k_) for o_, k_ in _shards(n, min(cores, n))]
     lim = _one_thread()
     # calibrate on the largest shard in this process
     off, k = shards[0]
-    o = _make(task, n, off, k, seed)
+    o = _make(task, n_total, off, k, seed)
     acts = np.random.RandomState(0).uniform(-1, 1, (4, k, 4))
     for j in range(2):
         o.step(acts[j])
@@ -137,7 +139,7 @@ def vectorised(task, n, seed=0, budget_s=3.0, cores=None):
     ctx = mp.get_context("fork")
     barrier = ctx.Barrier(len(shards))
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(task, n, o_, k_, seed, 2, steps, barrier, q)) for o_, k_ in shards]
+    procs = [ctx.Process(target=_worker, args=(task, n_total, o_, k_, seed, 2, steps, barrier, q)) for o_, k_ in shards]
     for p in procs:
         p.start()
     lim.unregister()
@@ -151,8 +153,9 @@ def vectorised(task, n, seed=0, budget_s=3.0, cores=None):
     wall = max(el)
     return {"task": task, "num_envs": n, "value": round(n * steps / wall, 1), "unit": "env-steps/s",
             "cores": len(shards), "steps": steps, "seconds": round(wall, 3),
-            "sample": f"oracle/quad_oracle.py OracleEnv float64 numpy, {task}, {n} envs in {len(shards)} "
-                      f"processes x {steps} steps ({wall:.2f} s)"}
+            "sample": f"f64 numpy restatement (oracle/quad_oracle.py OracleEnv), {task}, {n} envs"
+                      + (f" (global ids {env_id_offset}..{env_id_offset + n - 1} of {n_total})" if n_total != n else "")
+                      + f" in {len(shards)} processes x {steps} steps ({wall:.2f} s)"}
 
 
 def reference_structure(n=64, steps=None, seed=0, budget_s=2.0):

@@ -21,6 +21,7 @@
 
 #include "../../include/ouzelum.h"
 #include "quad_math.h"
+#include "quad_pv_ql.h"
 
 #define OUZ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
@@ -433,7 +434,8 @@ __device__ __forceinline__ void load_actions(const float* actions, EnvRegs<CTRL,
   }
 }
 
-template <int CTRL, int TGT, bool CLS = false, bool NTL = false>
+// QLN: the quad-lane estimator (quad_pv_ql.h): the PV covariance goes to LDS (pv_lds_load), not to registers.
+template <int CTRL, int TGT, bool CLS = false, bool NTL = false, bool QLN = false>
 __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskParams& tp, EnvRegs<CTRL, TGT>& S,
                                          const float* actions) {
   // reset_buf and time_outs are read unconditionally and combined without a branch, so the two flag
@@ -485,8 +487,10 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
     for (int k = 0; k < 10; ++k) S.eP[k] = L(OUZ_F_EKF_P + k);
 #pragma unroll
     for (int k = 0; k < 9; ++k) S.px[k] = L(OUZ_F_PV_X + k);
+    if constexpr (!QLN) {
 #pragma unroll
-    for (int k = 0; k < 45; ++k) S.pP[k] = L(OUZ_F_PV_P + k);
+      for (int k = 0; k < 45; ++k) S.pP[k] = L(OUZ_F_PV_P + k);
+    }
   }
   if constexpr (TGT == TGT_TRAJ) {
     S.plat = make_float2(L(OUZ_F_PLAT), L(OUZ_F_PLAT + 1));
@@ -499,7 +503,7 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   S.plat_v = make_float2(0.0f, 0.0f);
 }
 
-template <int CTRL, int TGT>
+template <int CTRL, int TGT, bool QLN = false>
 __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskParams& tp, const EnvRegs<CTRL, TGT>& S) {
   st3(S.T, OUZ_F_P, S.p);
   st(S.T, OUZ_F_Q, S.q.x); st(S.T, OUZ_F_Q + 1, S.q.y); st(S.T, OUZ_F_Q + 2, S.q.z); st(S.T, OUZ_F_Q + 3, S.q.w);
@@ -533,8 +537,10 @@ __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskPa
     for (int k = 0; k < 10; ++k) st(S.T, OUZ_F_EKF_P + k, S.eP[k]);
 #pragma unroll
     for (int k = 0; k < 9; ++k) st(S.T, OUZ_F_PV_X + k, S.px[k]);
+    if constexpr (!QLN) {
 #pragma unroll
-    for (int k = 0; k < 45; ++k) st(S.T, OUZ_F_PV_P + k, S.pP[k]);
+      for (int k = 0; k < 45; ++k) st(S.T, OUZ_F_PV_P + k, S.pP[k]);
+    }
   }
   if constexpr (TGT == TGT_TRAJ) {
     st(S.T, OUZ_F_PLAT, S.plat.x); st(S.T, OUZ_F_PLAT + 1, S.plat.y);
@@ -598,10 +604,11 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
 // ---------------------------------------------------------------------------
 // PRE: pre_physics_step only (ouz_pre_physics) -- stop before the integrator and write the body wrench
 // [6] (force, torque; body frame at the COM) that gym.simulate would integrate to `wrench`.
-template <int CTRL, int TGT, bool PRE = false>
+// QLN: the quad-lane estimator (four lanes per env, the PV covariance in LDS at `ql`).
+template <int CTRL, int TGT, bool PRE = false, bool QLN = false>
 __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
                                          EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout,
-                                         float* wrench = nullptr) {
+                                         float* wrench = nullptr, const PvQl* ql = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const EnvConsts& c = a.c;
   const bool rst = S.rst;
@@ -730,7 +737,12 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
-    {
+    if constexpr (QLN) {
+      // the covariance is in LDS and split over the env's lanes: no register peak to park around
+      pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u,
+                 v3(vm[0], vm[1], vm[2]));
+      OUZ_STAMP(12, false);
+    } else {
       // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
       // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
       // LDS around it (lane-contiguous slots: conflict-free) so those registers are free at the peak
@@ -976,22 +988,41 @@ struct LaneStats {
 
 // i: state slot (its wave tile is wave-uniform); e: env index (== i except under the trigger-class layout,
 // CLS), which keys the RNG and indexes the env-order buffers.
-template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false>
+// QLN: the quad-lane estimator (quad_pv_ql.h, latency-regime estimator kernels): the four lanes of a quad step
+// the same env (same slot i and env e) and split its PV covariance step; every other part of the step runs
+// identically in all four, and lane 0 of the quad alone writes the env's outputs, statistics and state
+// (the lanes 0-2 write the covariance elements they own).
+template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QLN = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
                                         bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
                                         float* wrench = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const uint32_t gid = a.env_offset + (uint32_t)e;
+  // the env's outputs / statistics / state writes: every lane, or lane 0 of the quad
+  const bool lead = QLN ? (threadIdx.x & 3u) == 0u : true;
+  const bool vout = valid && lead;
+  PvQl ql{};
+  if constexpr (QLN) {
+    static_assert(CTRL == CTRL_LEE_EST, "the quad-lane form is the estimator's");
+    __shared__ double s_pv[16 * kPvLdsEnv];   // one 64-lane block = one wave = 16 envs
+    const uint32_t sub = threadIdx.x & 3u;
+    double* env_lds = s_pv + (threadIdx.x >> 2) * kPvLdsEnv;
+    ql = PvQl{env_lds, env_lds + kPvLdsP, sub == 3u ? 0 : (int)sub, sub != 3u};
+  }
   EnvRegs<CTRL, TGT> S;
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT, CLS, NTL>(a, e, tp, S, ctx[0].actions);
+  if (valid) env_load<CTRL, TGT, CLS, NTL, QLN>(a, e, tp, S, ctx[0].actions);
+  if constexpr (QLN) {
+    if (valid) pv_lds_load(ql, [&](int f) { return ld(S.T, OUZ_F_PV_P + f); });
+    ql_sync();
+  }
   // fused statistics: the episode accumulators of earlier (unfused) steps, in flight with the state
   float ep_sum_old = 0.0f;
   int32_t ep_cnt_old = 0, ep_len_old = 0;
-  if (MULTI && stats_mode && valid) {
+  if (MULTI && stats_mode && vout) {
     ep_sum_old = ld(S.T, OUZ_F_EP_SUM);
     ep_cnt_old = ldi(S.T, OUZ_I_EP_CNT);
     ep_len_old = ldi(S.T, OUZ_I_EP_LEN);
@@ -1003,20 +1034,20 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
-    const bool did_reset = valid && S.rst;
-    if (valid) env_core<CTRL, TGT, true>(a, ctx[0], e, gid, task, S, ob, rew, rs, to, wrench);
+    const bool did_reset = vout && S.rst;
+    if (valid) env_core<CTRL, TGT, true, QLN>(a, ctx[0], e, gid, task, S, ob, rew, rs, to, wrench, &ql);
     if (did_reset) a.reset[e] = 0;
   } else if constexpr (!MULTI) {
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     bool rs = false, to = false;
-    const bool did_reset = valid && S.rst;
-    const bool flags_clear = valid && S.flags_clear;
-    if (valid) env_core<CTRL, TGT>(a, ctx[0], e, gid, task, S, ob, rew, rs, to);
+    const bool did_reset = vout && S.rst;
+    const bool flags_clear = vout && S.flags_clear;
+    if (valid) env_core<CTRL, TGT, false, QLN>(a, ctx[0], e, gid, task, S, ob, rew, rs, to, nullptr, &ql);
     trace_count(a, ctx[0].step, did_reset, i, e);
     OUZ_STAMP(5, false);
-    if (CLS) emit_env(outs[1], e, valid, ob, rew, rs, to, flags_clear);
-    else emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
+    if (CLS) emit_env(outs[1], e, vout, ob, rew, rs, to, flags_clear);
+    else emit(outs[1], wave_lds, i, a.n, vout, ob, rew, rs, to, direct, flags_clear);
     OUZ_STAMP(6, false);
   } else {
     // Drain the state loads before the step loop.  vmcnt counts loads and stores in one in-order counter,
@@ -1031,10 +1062,10 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       float ob[OUZ_NUM_OBS];
       float rew = 0.0f;
       bool rs = false, to = false;
-      const bool did_reset = valid && S.rst;
+      const bool did_reset = vout && S.rst;
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
-      const bool flags_clear = valid && (k == 0 ? S.flags_clear : !did_reset);
-      if (valid) env_core<CTRL, TGT>(a, ctx[k], e, gid, task, S, ob, rew, rs, to);
+      const bool flags_clear = vout && (k == 0 ? S.flags_clear : !did_reset);
+      if (valid) env_core<CTRL, TGT, false, QLN>(a, ctx[k], e, gid, task, S, ob, rew, rs, to, nullptr, &ql);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT, CLS>(ctx[k + 1].actions, S, e);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i, e);
@@ -1045,21 +1076,21 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
         o.reset += (size_t)k * out_stride;
         o.timeouts += (size_t)k * out_stride;
         if (CLS) {
-          emit_env(o, e, valid, ob, rew, rs, to, false);
-          if (k == K - 1) emit_env(outs[1], e, valid, ob, rew, rs, to, false);
+          emit_env(o, e, vout, ob, rew, rs, to, false);
+          if (k == K - 1) emit_env(outs[1], e, vout, ob, rew, rs, to, false);
         } else {
-          emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
-          if (k == K - 1) emit(outs[1], wave_lds, i, a.n, valid, ob, rew, rs, to, direct);
+          emit(o, wave_lds, i, a.n, vout, ob, rew, rs, to, direct);
+          if (k == K - 1) emit(outs[1], wave_lds, i, a.n, vout, ob, rew, rs, to, direct);
         }
       } else if (CLS) {
-        emit_env(o, e, valid, ob, rew, rs, to, flags_clear);
+        emit_env(o, e, vout, ob, rew, rs, to, flags_clear);
       } else {
-        emit(o, wave_lds, i, a.n, valid, ob, rew, rs, to, direct, flags_clear);
+        emit(o, wave_lds, i, a.n, vout, ob, rew, rs, to, direct, flags_clear);
       }
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
     }
     if (kStampSlots > 13 && K <= 16) OUZ_STAMP(13 + K, false);
-    if (stats_mode && valid) {
+    if (stats_mode && vout) {
       // RecordEpisodeStatisticsTorch over the rollout (PPO/utils.py:20-35) without a separate launch: this
       // lane's totals (accumulated before + finished in these K steps, same f32 adds as the atomics of
       // env_store) go to the grid reduction; drained accumulators are zeroed, kept ones written back.
@@ -1082,7 +1113,10 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       S.ep_cnt_add = 0;   // env_store: no accumulator atomics
     }
   }
-  if (valid) env_store<CTRL, TGT>(a, i, tp, S);
+  if (vout) env_store<CTRL, TGT, QLN>(a, i, tp, S);
+  if constexpr (QLN) {
+    if (valid) pv_lds_store(ql, [&](int f, float v) { st(S.T, OUZ_F_PV_P + f, v); });
+  }
   OUZ_STAMP(7, true);
   OUZ_STAMP_RT(9);
 }
@@ -1138,10 +1172,10 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Grid reduction of the lanes' episode statistics (see RolloutStats).  Called once per live wave.
-__device__ __forceinline__ void reduce_stats(const RolloutStats& rs, int n, int first, const LaneStats& ls) {
+// Grid reduction of the lanes' episode statistics (see RolloutStats).  Called once by each of the nw live waves
+// (w = its index in 0..nw-1, the partials' fixed summation order).
+__device__ __forceinline__ void reduce_stats(const RolloutStats& rs, uint32_t w, uint32_t nw, const LaneStats& ls) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t w = (uint32_t)first >> 6, nw = (uint32_t)(n + 63) >> 6;
   const double s = wave_sum(ls.sum), c = wave_sum(ls.cnt), l = wave_sum(ls.len);
   uint32_t last = 0;
   if (lane == 0u) {
@@ -1169,12 +1203,59 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, int n, int 
   }
 }
 
+// The quad-lane estimator (quad_pv_ql.h) runs the trigger-class layout of the estimator tasks and the
+// QuadTracking chunks of the mixed curriculum's class layout: 64-lane blocks (the latency regime), four per
+// 64-slot tile, each wave stepping 16 envs with 4 lanes each (quad_grid_blocks on the host).
+__host__ __device__ constexpr bool quad_lane_kernel(int task, bool cls) {
+  return cls && (task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING || task == OUZ_TASK_MIXED);
+}
+
 template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
   __shared__ float4 s_obs4[kMaxBlock * OUZ_NUM_OBS / 4];
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
+  const int sm = (MULTI && rst) ? rst->mode : 0;
+  LaneStats ls{0.0, 0.0, 0.0};
+  if constexpr (quad_lane_kernel(TASK, CLS)) {
+    // 64-lane blocks, four per tile: quarter q of tile t holds slots t*64 + q*16 .. +15, four lanes per slot
+    const int tile = (int)(blockIdx.x >> 2), quarter = (int)(blockIdx.x & 3u);
+    const int iq = tile * 64 + quarter * 16 + (int)(threadIdx.x >> 2);   // this quad's slot
+    bool quad = true;
+    int i = iq;
+    if constexpr (TASK == OUZ_TASK_MIXED) {
+      // a tile lies in one 1344-id chunk (one task): the QuadTracking chunks run quad-lane, the other tasks
+      // one lane per slot in the tile's first block (its other three exit at once)
+      const uint32_t ch = a.env_offset / kClassBlock + (uint32_t)(tile * 64) / kClassBlock;
+      quad = mixed_chunk_task(ch) == OUZ_TASK_TRACKING;
+      if (!quad) i = tile * 64 + (int)threadIdx.x;
+    }
+    int e = a.n;
+    if constexpr (TASK == OUZ_TASK_MIXED) {
+      const int64_t e64 = mixed_slot_env(a.env_offset, i);
+      e = (e64 >= 0 && e64 < a.n) ? (int)e64 : a.n;
+    } else {
+      e = slot_env(i);
+    }
+    const bool valid = e < a.n && (quad || quarter == 0);
+    if (quad) {
+      run_env<CTRL_LEE_EST, TASK == OUZ_TASK_EKF_LEE_LANDED ? TGT_PLATFORM : TGT_TRAJ, MULTI, PRE, true, false, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                      TASK == OUZ_TASK_MIXED ? OUZ_TASK_TRACKING : TASK, false, sm, &ls, wrench);
+    } else if (quarter == 0) {
+      if constexpr (TASK == OUZ_TASK_MIXED) {
+        const uint32_t ch = a.env_offset / kClassBlock + (uint32_t)(tile * 64) / kClassBlock;
+        if (mixed_chunk_task(ch) == OUZ_TASK_LEE_LANDED)
+          run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                               OUZ_TASK_LEE_LANDED, false, sm, &ls, wrench);
+        else
+          run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                     OUZ_TASK_FAULT, false, sm, &ls, wrench);
+      }
+    }
+    if (sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // every wave of the exact grid takes part
+    return;
+  }
   const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
   const int first = i - (int)(threadIdx.x & 63);
   if (first >= (CLS ? a.n_slots : a.n)) return;   // whole wave past the end
@@ -1186,8 +1267,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     e = slot_env(i);
   }
   const bool valid = e < a.n;
-  const int sm = (MULTI && rst) ? rst->mode : 0;
-  LaneStats ls{0.0, 0.0, 0.0};
   if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT) {
     run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_LEE_LANDED) {
@@ -1198,19 +1277,6 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
     run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
-  } else if constexpr (CLS) {
-    // mixed curriculum, class layout: a wave's slots lie in one 1344-id chunk, so its task is wave-uniform
-    const uint32_t c = a.env_offset / kClassBlock + __builtin_amdgcn_readfirstlane((uint32_t)first) / kClassBlock;
-    const int t = mixed_chunk_task(c);
-    if (t == OUZ_TASK_LEE_LANDED)
-      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
-                                                           OUZ_TASK_LEE_LANDED, false, sm, &ls, wrench);
-    else if (t == OUZ_TASK_TRACKING)
-      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
-                                                      OUZ_TASK_TRACKING, false, sm, &ls, wrench);
-    else
-      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_FAULT,
-                                                 false, sm, &ls, wrench);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -1229,7 +1295,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
       run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
                                         direct, sm, &ls, wrench);
   }
-  if (sm) reduce_stats(*rst, CLS ? a.n_slots : a.n, first, ls);
+  if (sm) reduce_stats(*rst, (uint32_t)first >> 6, (uint32_t)(a.n + 63) >> 6, ls);
 }
 
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
@@ -1793,10 +1859,11 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
   r = hip_check(hipMalloc(&e->drn_dev, 2 * sizeof(ouz_dr_noise)), "hipMalloc(dr noise)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
-  const size_t n_tiles = (size_t)OUZ_TILES(state_slots(cfg->task, cfg->num_envs));
-  r = hip_check(hipMalloc(&e->wave_partials, n_tiles * 3 * sizeof(double) + 64), "hipMalloc(wave partials)");
+  // one partial per wave of the rollout grid: four per tile under the quad-lane class layout
+  const size_t n_waves = (size_t)OUZ_TILES(state_slots(cfg->task, cfg->num_envs)) * 4;
+  r = hip_check(hipMalloc(&e->wave_partials, n_waves * 3 * sizeof(double) + 64), "hipMalloc(wave partials)");
   if (r) { (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
-  e->wave_ticket = reinterpret_cast<uint32_t*>(e->wave_partials + n_tiles * 3);
+  e->wave_ticket = reinterpret_cast<uint32_t*>(e->wave_partials + n_waves * 3);
   r = hip_check(hipMemset(e->wave_ticket, 0, sizeof(uint32_t)), "hipMemset(wave ticket)");
   if (r) { (void)hipFree(e->wave_partials); (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials);
            (void)hipFree(e->wp_tab); delete e; return r; }
@@ -1936,9 +2003,10 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
     }
   }
   if constexpr (class_layout_task(T)) {
-    if (a.cls) {
-      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g, b, 0, s, a, r.ctx[0]);
-      else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g, b, 0, s, a, r);
+    if (a.cls) {   // the quad-lane grid: four 64-lane blocks per 64-slot tile (step_body)
+      const dim3 g4(g.x * 4);
+      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g4, b, 0, s, a, r.ctx[0]);
+      else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g4, b, 0, s, a, r);
       return;
     }
   }
@@ -2122,22 +2190,23 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
   const int n = env->cfg.num_envs, blk = block_for(n);
   StepCtx c{(uint32_t)env->step, cached_flicker_mask(env, env->step), actions};
   dim3 g(grid_for(a.n_slots, blk)), b(blk);
+  const dim3 g4(g.x * 4);   // the quad-lane grid of the class layout (step_body)
   hipStream_t s = (hipStream_t)stream;
   switch (env->cfg.task) {
     case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_EKF_LEE_LANDED:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true>), g, b, 0, s, a, c, wrench);
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true>), g4, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, false>), g, b, 0, s, a, c, wrench);
       break;
     case OUZ_TASK_TRACKING:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true>), g, b, 0, s, a, c, wrench);
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true>), g4, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, false>), g, b, 0, s, a, c, wrench);
       break;
     case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LANDING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LANDING>, g, b, 0, s, a, c, wrench); break;
     default:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true>), g, b, 0, s, a, c, wrench);
+      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true>), g4, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, false>), g, b, 0, s, a, c, wrench);
       break;
   }

@@ -80,19 +80,6 @@ OUZ_HD M3T<T> tr(const M3T<T>& A) {
     for (int j = 0; j < 3; ++j) C.m[i * 3 + j] = A.m[j * 3 + i];
   return C;
 }
-template <typename T>
-OUZ_HD M3T<T> madd(const M3T<T>& A, const M3T<T>& B) { M3T<T> C;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] + B.m[k]; return C; }
-template <typename T>
-OUZ_HD M3T<T> msub(const M3T<T>& A, const M3T<T>& B) { M3T<T> C;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) C.m[k] = A.m[k] - B.m[k]; return C; }
-template <typename T>
-OUZ_HD M3T<T> mscale(T s, const M3T<T>& A) { M3T<T> C;
-#pragma unroll
-  for (int k = 0; k < 9; ++k) C.m[k] = s * A.m[k]; return C; }
-
 // 1 / x.  On the device, f64: the hardware reciprocal estimate refined by two Newton steps (full
 // double precision for the normal, positive determinants of SPD 3x3 blocks) instead of the
 // correctly rounded division sequence (div_scale / div_fmas / div_fixup), ~2x fewer f64 issues.
@@ -106,56 +93,6 @@ OUZ_HD T recip(T x) {
   }
 #endif
   return T(1) / x;
-}
-
-// Accumulating products, each entry ONE fma chain seeded with the accumulator: C + A B, C + A B^T and
-// C - A B.  (madd(C, mm(A, B)) is a mul, two fmas and an add per entry: the compiler may not
-// reassociate the add into the chain.)
-template <typename T>
-OUZ_HD M3T<T> mm_add(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
-  M3T<T> R;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      R.m[i * 3 + j] = fma(A.m[i * 3 + 2], B.m[2 * 3 + j], fma(A.m[i * 3 + 1], B.m[1 * 3 + j],
-                           fma(A.m[i * 3 + 0], B.m[0 * 3 + j], C.m[i * 3 + j])));
-  return R;
-}
-template <typename T>
-OUZ_HD M3T<T> mmt_add(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
-  M3T<T> R;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      R.m[i * 3 + j] = fma(A.m[i * 3 + 2], B.m[j * 3 + 2], fma(A.m[i * 3 + 1], B.m[j * 3 + 1],
-                           fma(A.m[i * 3 + 0], B.m[j * 3 + 0], C.m[i * 3 + j])));
-  return R;
-}
-template <typename T>
-OUZ_HD M3T<T> mm_sub(const M3T<T>& C, const M3T<T>& A, const M3T<T>& B) {
-  M3T<T> R;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      R.m[i * 3 + j] = fma(-A.m[i * 3 + 2], B.m[2 * 3 + j], fma(-A.m[i * 3 + 1], B.m[1 * 3 + j],
-                           fma(-A.m[i * 3 + 0], B.m[0 * 3 + j], C.m[i * 3 + j])));
-  return R;
-}
-template <typename T>
-OUZ_HD M3T<T> diag3(T d) { return M3T<T>{{d, T(0), T(0), T(0), d, T(0), T(0), T(0), d}}; }
-
-// Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).
-template <typename T>
-OUZ_HD M3T<T> inv_sym3(const M3T<T>& S) {
-  T a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
-  T A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
-  T D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
-  T inv_det = recip<T>(a * A + b * B + c * C);
-  return M3T<T>{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
-                 C * inv_det, E * inv_det, F * inv_det}};
 }
 
 // ---------------------------------------------------------------------------
@@ -458,125 +395,228 @@ OUZ_HD constexpr int s9(int i, int j) {
   return (i <= j) ? (i * 9 - (i * (i - 1)) / 2 + (j - i)) : (j * 9 - (j * (j - 1)) / 2 + (i - j));
 }
 
-// 3x3 block (bi, bj) of the packed 9x9 (bi, bj in 0..2).
-template <typename T>
-OUZ_HD M3T<T> pblk(const T P[45], int bi, int bj) {
-  M3T<T> B;
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) B.m[i * 3 + j] = P[s9(bi * 3 + i, bj * 3 + j)];
-  return B;
-}
-// Store block (bi <= bj); for a diagonal block only its upper triangle is kept.
-template <typename T>
-OUZ_HD void pset(T P[45], int bi, int bj, const M3T<T>& B) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      if (bi != bj || i <= j) P[s9(bi * 3 + i, bj * 3 + j)] = B.m[i * 3 + j];
-}
-
 constexpr float kPvAccVar = 1.0f;     // [0.01]*3 * 100 (ekf_lee_landed.py:137)
 constexpr float kPvPosVar = 1e-7f;    // ekf_lee_landed.py:408
 constexpr float kPvP0 = 1000.0f;      // PVFilter.py:12
 
-// prediction_step: M = R(q/|q|)^T; F = [[I, M dt, M h],[0, M, M dt],[0,0,I]], G = F[:, 6:9] (rows 0..5),
-// x = F x + G (a - b); P = F P F^T + q_a G G^T.   (h = dt^2/2)
-// Block form, P = [[A, B, C], [B^T, D, E], [C^T, E^T, Fb]]:
-//   T13 = C + M (dt E + h Fb)   T12 = B + M (dt D + h E^T)   T11 = A + M (dt B^T + h C^T)
-//   T23 = M (E + dt Fb)         T22 = M (D + dt E^T)
-//   A' = T11 + (dt T12 + h T13) M^T + q h^2 M M^T     B' = (T12 + dt T13) M^T + q h dt M M^T
-//   D' = (T22 + dt T23) M^T + q dt^2 M M^T             C' = T13, E' = T23, Fb' = Fb
-// M is formed in f32 from the f32 quaternion (as the reference's torch f32 does); the
-// covariance arithmetic runs in T.
+// The PV step's element formulas.  Every entry the step computes is ONE chain of explicit
+// fmas in a fixed order, written once below and evaluated by two data layouts:
+//  * the one-lane form (pv_predict_t / pv_correct_t): the packed covariance in one lane's registers -- the
+//    large-N step kernels and the component entries;
+//  * the quad-lane form (quad_pv_ql.h): the four lanes of an env split every 3x3 block by column, the full
+//    symmetric covariance in LDS -- the latency-regime estimator kernels.
+// Both take the same operations on the same operands for every stored element, so they agree bit for bit
+// (contraction is off here: a * b + c is never fused behind the formulas' back).
 template <typename T>
-OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
-  float inv = 1.0f / sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+OUZ_HD T dot3(T a0, T a1, T a2, T b0, T b1, T b2) {   // a . b, the a0 * b0 product seeding the chain
+#pragma clang fp contract(off)
+  return fma(a2, b2, fma(a1, b1, a0 * b0));
+}
+template <typename T>
+OUZ_HD T dot3s(T a0, T a1, T a2, T b0, T b1, T b2, T seed) {   // seed + a . b
+#pragma clang fp contract(off)
+  return fma(a2, b2, fma(a1, b1, fma(a0, b0, seed)));
+}
+
+// Inverse of a symmetric 3x3 via the adjugate (SPD inputs only).  Reads only the upper triangle.
+template <typename T>
+OUZ_HD M3T<T> inv_sym3(const M3T<T>& S) {
+#pragma clang fp contract(off)
+  const T a = S.m[0], b = S.m[1], c = S.m[2], d = S.m[4], e = S.m[5], f = S.m[8];
+  const T A = fma(d, f, -(e * e)), B = fma(c, e, -(b * f)), C = fma(b, e, -(c * d));
+  const T D = fma(a, f, -(c * c)), E = fma(b, c, -(a * e)), F = fma(a, d, -(b * b));
+  const T inv_det = recip<T>(fma(c, C, fma(b, B, a * A)));
+  return M3T<T>{{A * inv_det, B * inv_det, C * inv_det, B * inv_det, D * inv_det, E * inv_det,
+                 C * inv_det, E * inv_det, F * inv_det}};
+}
+
+// M = R(q/|q|)^T, formed in f32 from the f32 quaternion as the reference's torch f32 does (PVFilter.py:31-35)
+template <typename T>
+OUZ_HD M3T<T> pv_rot(EkfQ q) {
+  const float inv = 1.0f / sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
   const M3 Mf = tr(quat_to_mat(Q4{q.x * inv, q.y * inv, q.z * inv, q.w * inv}));
   M3T<T> M;
 #pragma unroll
   for (int k = 0; k < 9; ++k) M.m[k] = (T)Mf.m[k];
-  const T h = dt * dt * T(0.5);
-  {
-    T a1[3], a2[3], o[3];
+  return M;
+}
+
+// prediction_step, state part: x = F x + G (a - b), F = [[I, M dt, M h],[0, M, M dt],[0, 0, I]], h = dt^2 / 2
+template <typename T>
+OUZ_HD void pv_state_predict(T x[9], const T acc[3], const M3T<T>& M, T dt, T h) {
+#pragma clang fp contract(off)
+  T a1[3], a2[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      T u = acc[k] - x[6 + k];
-      a1[k] = dt * x[3 + k] + h * x[6 + k] + h * u;   // -> position
-      a2[k] = x[3 + k] + dt * x[6 + k] + dt * u;      // -> velocity
+  for (int k = 0; k < 3; ++k) {
+    const T u = acc[k] - x[6 + k];
+    a1[k] = fma(h, u, fma(dt, x[3 + k], h * x[6 + k]));   // -> position
+    a2[k] = fma(dt, u, fma(dt, x[6 + k], x[3 + k]));      // -> velocity
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) x[i] += dot3(M.m[i * 3], M.m[i * 3 + 1], M.m[i * 3 + 2], a1[0], a1[1], a1[2]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) x[3 + i] = dot3(M.m[i * 3], M.m[i * 3 + 1], M.m[i * 3 + 2], a2[0], a2[1], a2[2]);
+}
+
+// prediction_step, covariance part, P' = F P F^T + q_a G G^T, by columns.  With X_{r,b} the 3x3 blocks of P and
+// G_{r,b} = (F P)_{r,b}:  G_{0,b} = X_{0,b} + M (dt X_{1,b} + h X_{2,b}),  G_{1,b} = M (X_{1,b} + dt X_{2,b}),
+// G_{2,b} = X_{2,b};  then with Z00 = dt G_{0,1} + h G_{0,2}, Z01 = G_{0,1} + dt G_{0,2}, Z11 = G_{1,1} + dt G_{1,2}:
+//   P'_00 = G_{0,0} + Z00 M^T + q h^2 I,   P'_01 = Z01 M^T + q h dt I,   P'_11 = Z11 M^T + q dt^2 I,
+//   P'_02 = G_{0,2},   P'_12 = G_{1,2},   P'_22 = X_{2,2}
+// (G Q G^T = q_a [[h^2 M M^T, h dt M M^T], [dt h M M^T, dt^2 M M^T]] with M M^T = I up to M's f32 rounding,
+// the same as in the reference's own f32 product: the noise is diagonal).  Column c of G_{r,b} needs only
+// column c of the blocks (r, b): the quad-lane form computes its column locally and exchanges the Z's.
+template <typename T>
+OUZ_HD void pvf_g0(const M3T<T>& M, const T X0[3], const T X1[3], const T X2[3], T dt, T h, T out[3]) {
+#pragma clang fp contract(off)
+  T s[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = fma(dt, X1[k], h * X2[k]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out[i] = dot3s(M.m[i * 3], M.m[i * 3 + 1], M.m[i * 3 + 2], s[0], s[1], s[2], X0[i]);
+}
+template <typename T>
+OUZ_HD void pvf_g1(const M3T<T>& M, const T X1[3], const T X2[3], T dt, T out[3]) {
+#pragma clang fp contract(off)
+  T s[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) s[k] = fma(dt, X2[k], X1[k]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out[i] = dot3(M.m[i * 3], M.m[i * 3 + 1], M.m[i * 3 + 2], s[0], s[1], s[2]);
+}
+// column c of Z00, Z01, Z11 from column c of G_{0,1}, G_{0,2}, G_{1,1}, G_{1,2}
+template <typename T>
+OUZ_HD void pvf_z(const T g01[3], const T g02[3], const T g11[3], const T g12[3], T dt, T h, T z00[3], T z01[3],
+                  T z11[3]) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    z00[i] = fma(dt, g01[i], h * g02[i]);
+    z01[i] = fma(dt, g02[i], g01[i]);
+    z11[i] = fma(dt, g12[i], g11[i]);
+  }
+}
+
+template <typename T>
+OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
+  const M3T<T> M = pv_rot<T>(q);
+  const T h = dt * dt * T(0.5);
+  pv_state_predict(x, acc, M, dt, h);
+  const T q_a = (T)kPvAccVar, qhh = q_a * h * h, qhd = q_a * h * dt, qdd = q_a * dt * dt;
+  // every G column from the old P before anything is written: g[b][c][i] = G_{0,b}[i][c], g1[b-1][c][i] = G_{1,b}
+  T g0[3][3][3], g1[2][3][3];
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      T X0[3], X1[3], X2[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        X0[k] = P[s9(k, 3 * b + c)];
+        X1[k] = P[s9(3 + k, 3 * b + c)];
+        X2[k] = P[s9(6 + k, 3 * b + c)];
+      }
+      pvf_g0(M, X0, X1, X2, dt, h, g0[b][c]);
+      if (b > 0) pvf_g1(M, X1, X2, dt, g1[b - 1][c]);
     }
-    mva(M, a1, o);
-    x[0] += o[0]; x[1] += o[1]; x[2] += o[2];
-    mva(M, a2, o);
-    x[3] = o[0]; x[4] = o[1]; x[5] = o[2];
+  T z00[3][3], z01[3][3], z11[3][3];   // [column][row]
+#pragma unroll
+  for (int c = 0; c < 3; ++c) pvf_z(g0[1][c], g0[2][c], g1[0][c], g1[1][c], dt, h, z00[c], z01[c], z11[c]);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const T m0 = M.m[c * 3], m1 = M.m[c * 3 + 1], m2 = M.m[c * 3 + 2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i <= c) P[s9(i, c)] = dot3s(z00[0][i], z00[1][i], z00[2][i], m0, m1, m2, i == c ? g0[0][c][i] + qhh : g0[0][c][i]);
+      P[s9(i, 3 + c)] = dot3s(z01[0][i], z01[1][i], z01[2][i], m0, m1, m2, i == c ? qhd : T(0));
+      if (i <= c) P[s9(3 + i, 3 + c)] = dot3s(z11[0][i], z11[1][i], z11[2][i], m0, m1, m2, i == c ? qdd : T(0));
+      P[s9(i, 6 + c)] = g0[2][c][i];
+      P[s9(3 + i, 6 + c)] = g1[1][c][i];
+    }
   }
-  const T q_a = (T)kPvAccVar;
-  // G Q Gᵀ = q_a [[h² M Mᵀ, h dt M Mᵀ], [dt h M Mᵀ, dt² M Mᵀ]] with M a rotation: M Mᵀ = I up to the
-  // f32 rounding of M (~1e-7, the same as in the reference's own f32 product), so the noise term is
-  // diagonal (diag3 below) and the 27-FMA f64 product is not formed.
-  M3T<T> T13 = mm_add(pblk(P, 0, 2), M, madd(mscale(dt, pblk(P, 1, 2)), mscale(h, pblk(P, 2, 2))));
-  M3T<T> T12 = mm_add(pblk(P, 0, 1), M, madd(mscale(dt, pblk(P, 1, 1)), mscale(h, pblk(P, 2, 1))));
-  {
-    M3T<T> T11 = mm_add(pblk(P, 0, 0), M, madd(mscale(dt, pblk(P, 1, 0)), mscale(h, pblk(P, 2, 0))));
-    pset(P, 0, 0, mmt_add(madd(T11, diag3(q_a * h * h)), madd(mscale(dt, T12), mscale(h, T13)), M));
-  }
-  pset(P, 0, 1, mmt_add(diag3(q_a * h * dt), madd(T12, mscale(dt, T13)), M));
-  M3T<T> T23 = mm(M, madd(pblk(P, 1, 2), mscale(dt, pblk(P, 2, 2))));
-  M3T<T> T22 = mm(M, madd(pblk(P, 1, 1), mscale(dt, pblk(P, 2, 1))));
-  pset(P, 1, 1, mmt_add(diag3(q_a * dt * dt), madd(T22, mscale(dt, T23)), M));
-  pset(P, 0, 2, T13);
-  pset(P, 1, 2, T23);
 }
 
 // correction_step for one measured block m (0 = position, 1 = velocity) with R = r I.
-// Stable form of x += K (z - x_m); P = (I - K H) P  (DESIGN.md §4):
-//   S = P_mm + r I;  K_o = P_om S^-1 (o != m)
-//   x_m = z - r S^-1 y;  x_o += K_o y
-//   P_mm = r (I - r S^-1);  P_mo = r S^-1 P_mo = r K_o^T;  P_oo' = P_oo' - K_o P_mo'
-// R0 = true: the velocity fix as the reference runs it, R = 0 (PVFilter.py:76-79 tests gps_var): the
-// r-scaled terms are exact zeros (x_m = z, P_mm = P_mo = 0), written as zeros instead of computed as
-// 0 * (products) — IEEE f64 cannot fold 0 * x, so the generic form pays ~40 f64 operations for them.
+// Stable form of x += K (z - x_m); P = (I - K H) P  (DESIGN.md §4), the other blocks A < B:
+//   S = P_mm + r I;  K_o = P_om S^-1;  x_m = z - r S^-1 y;  x_o += K_o y   (y = z - x_m)
+//   P_oo' = P_oo' - K_o P_mo';  P_mo = r K_o^T;  P_mm = r (I - r S^-1)
+// R0 = true: the velocity fix as the reference runs it, R = 0 (PVFilter.py:76-79 tests gps_var): x_m = z and
+// P_mm = P_mo = 0, written as zeros (IEEE f64 cannot fold 0 * x).
+// Row i of K_o = row i of P_om times S^-1; element (i, c) of an updated block = seed - (row i of K) . (column c
+// of P_mo); the quad-lane form computes row c of each K and column c of each block.
 template <int MB, typename T, bool R0 = false>
 OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
+#pragma clang fp contract(off)
   constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
   constexpr int B = 2;
-  M3T<T> Si;
+  M3T<T> S;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) S.m[i * 3 + j] = P[s9(3 * MB + i, 3 * MB + j)];
+  S.m[0] += r; S.m[4] += r; S.m[8] += r;
+  const M3T<T> Si = inv_sym3(S);
+  T KA[3][3], KB[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      KA[i][j] = dot3(P[s9(3 * A + i, 3 * MB)], P[s9(3 * A + i, 3 * MB + 1)], P[s9(3 * A + i, 3 * MB + 2)],
+                      Si.m[j], Si.m[3 + j], Si.m[6 + j]);
+      KB[i][j] = dot3(P[s9(3 * B + i, 3 * MB)], P[s9(3 * B + i, 3 * MB + 1)], P[s9(3 * B + i, 3 * MB + 2)],
+                      Si.m[j], Si.m[3 + j], Si.m[6 + j]);
+    }
   {
-    M3T<T> S = pblk(P, MB, MB);
-    S.m[0] += r; S.m[4] += r; S.m[8] += r;
-    Si = inv_sym3(S);
-  }
-  const M3T<T> KA = mm(pblk(P, A, MB), Si), KB = mm(pblk(P, B, MB), Si);     // K_o = P_{o,m} S^-1
-  {
-    T y[3] = {z[0] - x[MB * 3 + 0], z[1] - x[MB * 3 + 1], z[2] - x[MB * 3 + 2]};
-    T sy[3] = {T(0), T(0), T(0)}, dA[3], dB[3];
-    if constexpr (!R0) mva(Si, y, sy);
-    mva(KA, y, dA);
-    mva(KB, y, dB);
+    T y[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) y[k] = z[k] - x[MB * 3 + k];
+    T xm[3], dA[3], dB[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      xm[i] = R0 ? z[i] : fma(-r, dot3(Si.m[i * 3], Si.m[i * 3 + 1], Si.m[i * 3 + 2], y[0], y[1], y[2]), z[i]);
+      dA[i] = dot3(KA[i][0], KA[i][1], KA[i][2], y[0], y[1], y[2]);
+      dB[i] = dot3(KB[i][0], KB[i][1], KB[i][2], y[0], y[1], y[2]);
+    }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      x[MB * 3 + k] = R0 ? z[k] : z[k] - r * sy[k];
+      x[MB * 3 + k] = xm[k];
       x[A * 3 + k] += dA[k];
       x[B * 3 + k] += dB[k];
     }
   }
-  // other-other blocks first: they read P_{m,o}, which is overwritten below
-  pset(P, B, B, mm_sub(pblk(P, B, B), KB, pblk(P, MB, B)));
-  pset(P, A, B, mm_sub(pblk(P, A, B), KA, pblk(P, MB, B)));
-  pset(P, A, A, mm_sub(pblk(P, A, A), KA, pblk(P, MB, A)));
-  if constexpr (R0) {
-    const M3T<T> Z{{T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0), T(0)}};
-    if (MB < A) pset(P, MB, A, Z); else pset(P, A, MB, Z);
-    pset(P, MB, B, Z);
-    pset(P, MB, MB, Z);
-  } else {
-    if (MB < A) pset(P, MB, A, mscale(r, tr(KA))); else pset(P, A, MB, mscale(r, KA));
-    pset(P, MB, B, mscale(r, tr(KB)));
-    M3T<T> I3{{T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)}};
-    pset(P, MB, MB, mscale(r, msub(I3, mscale(r, Si))));
+  // the other-other blocks first: they read the m-row blocks, which are overwritten below
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const T pb0 = P[s9(3 * MB, 6 + c)], pb1 = P[s9(3 * MB + 1, 6 + c)], pb2 = P[s9(3 * MB + 2, 6 + c)];
+    const T pa0 = P[s9(3 * MB, 3 * A + c)], pa1 = P[s9(3 * MB + 1, 3 * A + c)], pa2 = P[s9(3 * MB + 2, 3 * A + c)];
+    T bb[3], ab[3], aa[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      bb[i] = dot3s(-KB[i][0], -KB[i][1], -KB[i][2], pb0, pb1, pb2, P[s9(6 + i, 6 + c)]);
+      ab[i] = dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pb0, pb1, pb2, P[s9(3 * A + i, 6 + c)]);
+      aa[i] = dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pa0, pa1, pa2, P[s9(3 * A + i, 3 * A + c)]);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i <= c) P[s9(6 + i, 6 + c)] = bb[i];
+      P[s9(3 * A + i, 6 + c)] = ab[i];
+      if (i <= c) P[s9(3 * A + i, 3 * A + c)] = aa[i];
+    }
   }
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if constexpr (R0) {
+        if (MB < A) P[s9(3 * MB + i, 3 * A + c)] = T(0); else P[s9(3 * A + i, 3 * MB + c)] = T(0);
+        P[s9(3 * MB + i, 6 + c)] = T(0);
+        if (i <= c) P[s9(3 * MB + i, 3 * MB + c)] = T(0);
+      } else {
+        if (MB < A) P[s9(3 * MB + i, 3 * A + c)] = r * KA[c][i]; else P[s9(3 * A + i, 3 * MB + c)] = r * KA[i][c];
+        P[s9(3 * MB + i, 6 + c)] = r * KB[c][i];
+        if (i <= c) P[s9(3 * MB + i, 3 * MB + c)] = r * fma(-r, Si.m[i * 3 + c], i == c ? T(1) : T(0));
+      }
+    }
 }
 
 // One PV-filter step as the driver runs it (ekf_lee_landed.py:417-444): predict, then the

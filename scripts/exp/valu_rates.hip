@@ -30,19 +30,33 @@ __global__ void __launch_bounds__(64) probe(float* out, double* outd, long long*
       f[0] = __builtin_fmaf(f[0], a, b);
     } else if constexpr (MODE == 3) {   // one dependent f64 chain
       d[0] = __builtin_fma(d[0], ad, bd);
-    } else if constexpr (MODE == 4) {   // 8 independent DPP quad_perm moves (b32) feeding adds
+    } else if constexpr (MODE == 4) {   // 8 independent DPP quad_perm moves (b32, bound_ctrl) feeding adds
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        int v = __builtin_amdgcn_update_dpp(0, __float_as_int(f[k]), 0x39 /*quad_perm [1,2,3,0]*/, 0xF, 0xF, false);
+        int v = __builtin_amdgcn_mov_dpp(__float_as_int(f[k]), 0x39 /*quad_perm [1,2,3,0]*/, 0xF, 0xF, true);
         f[k] = __int_as_float(v) + b;
       }
     } else if constexpr (MODE == 5) {   // 8 independent f64 DPP moves (two b32 DPP each) feeding f64 adds
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         long long x = __double_as_longlong(d[k]);
-        int lo = __builtin_amdgcn_update_dpp(0, (int)x, 0x39, 0xF, 0xF, false);
-        int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), 0x39, 0xF, 0xF, false);
+        int lo = __builtin_amdgcn_mov_dpp((int)x, 0x39, 0xF, 0xF, true);
+        int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), 0x39, 0xF, 0xF, true);
         d[k] = __longlong_as_double(((long long)hi << 32) | (unsigned)lo) + bd;
+      }
+    } else if constexpr (MODE == 9) {   // 24 DPP moves of 8 values computed long before (no hazard), summed
+      float g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f[k]), 0x39, 0xF, 0xF, true))
+                                     + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f[k]), 0x4E, 0xF, 0xF, true))
+                                     + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(f[k]), 0x93, 0xF, 0xF, true));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = __builtin_fmaf(f[k], a, g[k] * 1e-9f);
+    } else if constexpr (MODE == 10) {   // ds_swizzle quad_perm-like moves, 8 independent
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        int v = __builtin_amdgcn_ds_swizzle(__float_as_int(f[k]), 0x8039);
+        f[k] = __int_as_float(v) + b;
       }
     } else if constexpr (MODE == 6) {   // 8 independent f64 muls
 #pragma unroll
@@ -97,5 +111,7 @@ int main() {
   run<4>("DPP b32 move + f32 add, 8 independent (per pair)", 8);
   run<5>("f64 DPP (2 b32 DPP) + f64 add, 8 indep (per triple)", 8);
   run<7>("cvt f64->f32, add, cvt f32->f64, 8 indep (per triple)", 8);
+  run<9>("3 DPP of old values + 2 add + 1 fma (per 6)", 8);
+  run<10>("ds_swizzle + f32 add, 8 indep (per pair)", 8);
   return 0;
 }

@@ -1,17 +1,36 @@
 """Average FETCH_SIZE / WRITE_SIZE (KB) per quad_step_kernel (or quad_rollout_kernel) dispatch -> HBM bytes
-per launch.
+per launch, plus the kernel's average duration from a --kernel-trace --stats pass of the same workload.
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the bytes of wide
 coalesced streaming reads -> doubled; WRITE_SIZE is exact for 16-B streaming stores.
 Writes profiles-ready JSON next to the raw counters:
     python pmc_summarize.py OUTDIR TAG TASK N            (round-1 layout: pmc_TAG_TASK_N_*, step kernel)
-    python pmc_summarize.py OUTDIR TAG TASK N MODE       (scripts/gpu_pmc2.sh: pmc_TAG_MODE_TASK_N_*)
+    python pmc_summarize.py OUTDIR TAG TASK N MODE       (scripts/gpu_pmc2.sh / gpu_roofline_evidence.sh:
+                                                          pmc_TAG_MODE_TASK_N_*)
+A rollout of a task that streams it at this size (bench.py streamed_rollout) runs step kernels: its summary
+is the step kernel's.  ``lib_sha16``: the library the counters were taken on (bench.py only uses a summary of
+the library it loaded).
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_sha16(path=None):
+    path = path or os.environ.get("OUZ_LIB") or os.path.join(ROOT, "ouzelum_amd", "libouzelum_hip.so")
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
+def _hit(name, kernel):
+    # the single-step launch (quad_step_kernel<TASK>, or its large-N pipelined form quad_step_pipe_kernel<TASK>),
+    # not quad_rollout_kernel<TASK>
+    return kernel in name or (kernel == "quad_step_kernel<" and "quad_step_pipe_kernel<" in name)
 
 
 def avg_counter(path_glob, counter, kernel="quad_step_kernel<"):
@@ -19,25 +38,39 @@ def avg_counter(path_glob, counter, kernel="quad_step_kernel<"):
     for f in glob.glob(path_glob, recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                name = row.get("Kernel_Name", "")
-                # the single-step launch (quad_step_kernel<TASK>, or its large-N pipelined form
-                # quad_step_pipe_kernel<TASK>), not quad_rollout_kernel<TASK>
-                hit = kernel in name or (kernel == "quad_step_kernel<" and "quad_step_pipe_kernel<" in name)
-                if hit and row.get("Counter_Name") == counter:
+                if _hit(row.get("Kernel_Name", ""), kernel) and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def avg_duration_us(stats_dir, kernel):
+    """Average duration of the kernel from the rocprofv3 --stats kernel_stats.csv (ns -> us)."""
+    for f in glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if _hit(row.get("Name", ""), kernel):
+                    return float(row["AverageNs"]) / 1e3, int(row["Calls"]), os.path.relpath(f, stats_dir)
+    return None, 0, None
 
 
 def main():
     out, tag, task, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     mode = sys.argv[5] if len(sys.argv) > 5 else None
     base = os.path.join(out, f"pmc_{tag}_{mode}_{task}_{n}" if mode else f"pmc_{tag}_{task}_{n}")
-    kernel = "quad_rollout_kernel<" if mode == "rollout" else "quad_step_kernel<"
+    streamed = mode == "rollout" and n > 131072 and task not in ("EKFLeeLanded", "QuadTracking", "QuadMixed")
+    kernel = "quad_rollout_kernel<" if mode == "rollout" and not streamed else "quad_step_kernel<"
     fetch, nf = avg_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", kernel)
     write, nw = avg_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", kernel)
-    steps = 16 if mode == "rollout" else 1
+    steps = 16 if kernel == "quad_rollout_kernel<" else 1
     res = {"task": task, "num_envs": n, "kernel": kernel.rstrip("<"), "steps_per_launch": steps,
            "dispatches": [nf, nw], "fetch_size_kb_raw": fetch, "write_size_kb": write}
+    try:
+        res["lib_sha16"] = lib_sha16()
+    except OSError:
+        pass
+    us, calls, src = avg_duration_us(base + "_STATS", kernel)
+    if us is not None:
+        res.update({"rocprof_avg_us": us, "rocprof_calls": calls, "rocprof_stats_csv": src})
     if fetch is not None and write is not None:
         res["read_bytes_corrected"] = fetch * 1024 * 2
         res["write_bytes"] = write * 1024

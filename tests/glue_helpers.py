@@ -9,7 +9,7 @@ from oracle import quad_oracle as Q
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GLUE = {"ekf": "EKFLeeLanded", "ekf_flicker": "EKFLeeLanded", "lee": "LeeLanded", "ouz": "Ouzelum",
-        "landing": "Landing"}
+        "landing": "Landing", "ekf_conv300": "EKFLeeLanded"}
 PLAT_KEYS = ("plat", "plat_heading", "traj_type", "traj_idx", "traj_sd")
 
 
@@ -25,8 +25,18 @@ def oracle_config(name, fx, n=None):
                        if task not in ("Ouzelum", "Landing") else None)
 
 
+def step0(fx):
+    """Global step of the fixture's first recorded state (0 unless only the end of a long run was recorded)."""
+    return int(fx["step0"]) if "step0" in fx else 0
+
+
+def first_state(fx):
+    """First recorded state a single-step replay can start from (-1: the start state, before any step)."""
+    return -1 if step0(fx) == 0 else 0
+
+
 def state(fx, t, name):
-    """The env state after step t (t = -1: the fixture's start state), as the next step reads it."""
+    """The env state after recorded step t (t = -1: the fixture's start state), as the next step reads it."""
     n = fx["init_p"].shape[0]
     if t < 0:
         task_z = 1.0 if GLUE[name] == "Ouzelum" else 0.377
@@ -50,7 +60,7 @@ def state(fx, t, name):
     for k in PLAT_KEYS:
         if k in fx:
             st[k] = fx[k][t]
-    st["sim_step"] = t + 1
+    st["sim_step"] = t + 1 + step0(fx)
     return st
 
 

@@ -475,7 +475,10 @@ def initial_state(task, n, seed):
     return out
 
 
-def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
+def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8, record_from=0):
+    """``record_from``: record the states of steps >= record_from only (a long run whose interesting part is its
+    end, e.g. the 300-step convergence window of EKFLeeLanded.yaml:18); the fixture's ``step0`` says where the
+    recorded steps start, ``actions`` holds their actions and ``actions_all`` every step's."""
     D.seed, D.task = seed, TASK_IDS[task]
     e = make_env(mods, task, n, pomdp_prob, conv)
     s0 = initial_state(task, n, seed)
@@ -503,6 +506,9 @@ def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
         with contextlib.redirect_stdout(io.StringIO()):
             obs, rew, reset, extras = e.step(torch.tensor(acts[t]))
         assert not D.coins, f"{len(D.coins)} POMDP coins left: the call order changed"
+        if t < record_from:
+            rec["ekf_input_corrupted"].pop()
+            continue
         rs_ = e.root_states.numpy()
         rec["p"].append(rs_[:, 0:3].copy())
         rec["q"].append(rs_[:, 3:7].copy())
@@ -533,7 +539,10 @@ def run_task(mods, task, n, steps, seed, pomdp_prob=0.0, conv=8):
             rec["flag"].append(e.flag.numpy().copy())
     out = {f"init_{k}": np.asarray(v) for k, v in s0.items()}
     out.update({k: np.stack(v) for k, v in rec.items() if v})
-    out["actions"] = acts
+    out["actions"] = acts[record_from:]
+    if record_from:
+        out["actions_all"] = acts
+    out["step0"] = np.array(record_from)
     out["seed"] = np.array(seed)
     out["convergence_time"] = np.array(conv)
     out["pomdp_prob"] = np.array(pomdp_prob)
@@ -602,7 +611,9 @@ def run_pomdp(mods, seed=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma-separated fixture names to (re)write; default: all")
     a = ap.parse_args()
+    only = set(x for x in a.only.split(",") if x)
     torch.Tensor.to = _to_cpu
     mods = install_stubs(a.ref)
     cwd = os.getcwd()
@@ -612,16 +623,29 @@ def main():
         try:
             torch.set_default_dtype(torch.float64)
             res = {}
-            res["ekf"] = run_task(mods, "EKFLeeLanded", 42, 36, seed=5, pomdp_prob=0.0, conv=8)
-            res["ekf_flicker"] = run_task(mods, "EKFLeeLanded", 42, 24, seed=6, pomdp_prob=0.15, conv=6)
-            res["lee"] = run_task(mods, "LeeLanded", 40, 30, seed=7, pomdp_prob=0.2)
-            res["ouz"] = run_task(mods, "Ouzelum", 40, 30, seed=8)
-            res["landing"] = run_task(mods, "Landing", 48, 120, seed=9)
-            msg = ekf_input_corruption_raises(mods)
-            assert msg, "the reference no longer raises on a corrupted EKF input: revisit step_coins"
-            res["ekf_flicker"]["ekf_input_corruption_error"] = np.array(msg)
+            want = lambda k: not only or k in only   # noqa: E731
+            if want("ekf"):
+                res["ekf"] = run_task(mods, "EKFLeeLanded", 42, 36, seed=5, pomdp_prob=0.0, conv=8)
+            if want("ekf_flicker"):
+                res["ekf_flicker"] = run_task(mods, "EKFLeeLanded", 42, 24, seed=6, pomdp_prob=0.15, conv=6)
+            if want("lee"):
+                res["lee"] = run_task(mods, "LeeLanded", 40, 30, seed=7, pomdp_prob=0.2)
+            if want("ouz"):
+                res["ouz"] = run_task(mods, "Ouzelum", 40, 30, seed=8)
+            if want("landing"):
+                res["landing"] = run_task(mods, "Landing", 48, 120, seed=9)
+            # the task's own 300-step convergence window (EKFLeeLanded.yaml:18; ekf_lee_landed.py:339,526-530):
+            # 336 reference steps, the last 46 (steps 290-335) recorded
+            if want("ekf_conv300"):
+                res["ekf_conv300"] = run_task(mods, "EKFLeeLanded", 24, 336, seed=10, pomdp_prob=0.0, conv=300,
+                                              record_from=290)
+            if want("ekf_flicker"):
+                msg = ekf_input_corruption_raises(mods)
+                assert msg, "the reference no longer raises on a corrupted EKF input: revisit step_coins"
+                res["ekf_flicker"]["ekf_input_corruption_error"] = np.array(msg)
             torch.set_default_dtype(torch.float32)
-            res["pomdp"] = run_pomdp(mods)
+            if want("pomdp"):
+                res["pomdp"] = run_pomdp(mods)
         finally:
             os.chdir(cwd)
             torch.set_default_dtype(torch.float32)

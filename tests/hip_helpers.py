@@ -99,3 +99,30 @@ def quat_canon(q):
     """q and -q are the same rotation; align signs for comparison."""
     s = np.where(q[..., 3:4] < 0, -1.0, 1.0)
     return q * s
+
+
+def decision_margin(o, before, conv_time=300):
+    """Per env: distance of the oracle's state from the thresholds of the estimator tasks' discrete decisions,
+    where an f32 and an f64 run may legitimately take different branches (then their trajectories part).
+    before=True (the state the next step reads): landing cut 0.25 m and waypoint re-aim at 0.75 m of the
+    target, waypoint re-aim below 0.5 / above 1.0 m (ekf_lee_landed.py:476-515).  before=False (after the
+    step): die lines z 0.3 / distance 8 (:718), the landing deck (z 0.375 inside the chassis disk, DESIGN.md
+    §3), the husky's waypoint switch / heading dead band (oracle plat_margin)."""
+    if before:
+        # inside the convergence window the wrench is the fixed up-force whatever the guidance decides
+        # (ekf_lee_landed.py:526-530) and the waypoint is the target; an env with a pending reset steps from
+        # its reset pose, not from this state
+        if o.sim_step < conv_time:
+            return np.full(o.n, np.inf)
+        td = np.sqrt(((o.target - o.p) ** 2).sum(-1))
+        wd = np.sqrt(((o.waypoint - o.p) ** 2).sum(-1))
+        m = np.minimum(np.abs(td - 0.25), np.abs(td - 0.75))
+        m = np.minimum(m, np.minimum(np.abs(wd - 0.5), np.abs(wd - 1.0)))
+        return np.where(o.reset_buf != 0, np.inf, m)
+    d = np.sqrt(((o.target - o.p) ** 2).sum(-1))
+    m = np.minimum(np.abs(o.p[:, 2] - 0.3), np.abs(d - 8.0))
+    r2 = ((o.p[:, 0:2] - o.plat) ** 2).sum(-1)
+    deck = np.where(r2 < Q.DECK_RADIUS ** 2 + 1e-3, np.abs(o.p[:, 2] - Q.DECK_Z_REST), np.abs(r2 - Q.DECK_RADIUS ** 2))
+    m = np.minimum(m, deck)
+    pm = getattr(o, "plat_margin", None)
+    return m if pm is None else np.minimum(m, pm)

@@ -71,24 +71,28 @@ def compare(name, o, fx, t, mask=None):
         np.testing.assert_array_equal(a, b, err_msg=f"{name}@{t} {k}")
 
 
-@pytest.mark.parametrize("name", ["ekf", "lee", "ouz", "landing"])
+@pytest.mark.parametrize("name", ["ekf", "lee", "ouz", "landing", "ekf_conv300"])
 def test_glue_free_run(name):
     """The oracle started from the fixture's start state and stepped with its actions reproduces the reference's
-    whole trajectory (resets, time-outs, the convergence window, landings, random goals)."""
+    whole trajectory (resets, time-outs, the convergence window, landings, random goals).  ekf_conv300: 336 steps
+    with the task's own 300-step convergence window, compared over the recorded steps 290-335."""
     fx = G.load(name)
     o = Q.OracleEnv(G.oracle_config(name, fx))
     G.to_oracle(o, G.state(fx, -1, name))
-    for t in range(fx["p"].shape[0]):
-        o.step(fx["actions"][t])
-        compare(name, o, fx, t)
+    s0 = G.step0(fx)
+    acts = fx["actions_all"] if "actions_all" in fx else fx["actions"]
+    for t in range(s0 + fx["p"].shape[0]):
+        o.step(acts[t])
+        if t >= s0:
+            compare(name, o, fx, t - s0)
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing", "ekf_conv300"])
 def test_glue_single_step(name):
     """One oracle step from every recorded reference state (exclusions: see the module docstring)."""
     fx = G.load(name)
     n = fx["init_p"].shape[0]
-    for t in range(-1, fx["p"].shape[0] - 1):
+    for t in range(G.first_state(fx), fx["p"].shape[0] - 1):
         o = Q.OracleEnv(G.oracle_config(name, fx))
         G.to_oracle(o, G.state(fx, t, name))
         o.step(fx["actions"][t + 1])
@@ -111,6 +115,12 @@ def test_glue_fixtures_cover_the_branches():
     frac = f["ekf_input_corrupted"][int(f["convergence_time"]):].mean()
     assert 0.05 < frac < 0.3
     assert "unsupported operand" in str(f["ekf_input_corruption_error"])   # the reference's own TypeError
+    c = G.load("ekf_conv300")
+    s0, conv = G.step0(c), int(c["convergence_time"])
+    assert conv == 300 and s0 < conv < s0 + c["p"].shape[0] - 20           # the task's own window, crossed
+    fz = c["f_b"][:, :, 2]
+    assert np.allclose(fz[:conv - s0], 2.09 * 9.81 * 1.0) or (np.abs(fz[:conv - s0] - 2.09 * 9.81) < 1e-9).all()
+    assert (np.abs(fz[conv - s0:] - 2.09 * 9.81) > 1e-6).any()             # Lee control after the window
     assert (np.abs(lee["obs"]).sum((1, 2)) == 0).any()                  # LeeLanded flicker fired
     assert (ouz["progress"] % 500 == 0).any()                           # random goals redrawn
     assert np.abs(ouz["thrust"]).max() > 0

@@ -52,14 +52,14 @@ def near_threshold(fx, t, name):
     return (np.abs(d - 8.0) < 1e-4) | (np.abs(p[:, 2] - z_die) < 1e-4)
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing", "ekf_conv300"])
 def test_gpu_step_from_reference_states(ouz, name):
     from ouzelum_amd import _lib as L
     fx = G.load(name)
     env = make_env(ouz, name, fx)
     n = fx["init_p"].shape[0]
     ekf = G.GLUE[name] == "EKFLeeLanded"
-    for t in range(-1, fx["p"].shape[0] - 1):
+    for t in range(G.first_state(fx), fx["p"].shape[0] - 1):
         G.to_gpu(env, G.state(fx, t, name))
         env.step(torch.as_tensor(fx["actions"][t + 1], dtype=torch.float32, device="cuda"))
         torch.cuda.synchronize()
@@ -97,7 +97,7 @@ def test_gpu_step_from_reference_states(ouz, name):
             assert m.sum() > n // 2
 
 
-@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing"])
+@pytest.mark.parametrize("name", ["ekf", "ekf_flicker", "lee", "ouz", "landing", "ekf_conv300"])
 def test_gpu_pre_physics_wrench(ouz, name):
     """ouz_pre_physics from every recorded state: the body wrench the reference applied in the next step, and
     (EKF task) the filter / waypoint state its pre_physics_step left."""
@@ -105,7 +105,7 @@ def test_gpu_pre_physics_wrench(ouz, name):
     fx = G.load(name)
     env = make_env(ouz, name, fx)
     ekf = G.GLUE[name] == "EKFLeeLanded"
-    for t in range(-1, fx["p"].shape[0] - 1):
+    for t in range(G.first_state(fx), fx["p"].shape[0] - 1):
         st = G.state(fx, t, name)
         G.to_gpu(env, st)
         wr = env.pre_physics(torch.as_tensor(fx["actions"][t + 1], dtype=torch.float32, device="cuda"))
