@@ -303,6 +303,10 @@ int ouz_pv_correct(float* x9, float* P45, const float* z, int32_t block, float v
                    int32_t n, void* stream);
 int ouz_pv_step(float* x9, float* P45, const float* acc, const float* q_wxyz, float dt, const float* pos_z,
                 const uint8_t* pos_mask, const float* vel_z, const uint8_t* vel_mask, int32_t n, void* stream);
+/* ouz_pv_step in the quad-lane form of the latency-regime estimator kernels (four lanes per env, the
+ * covariance in LDS; quad_pv_ql.h): the same results bit for bit (tests/test_gpu_components.py). */
+int ouz_pv_step_quad(float* x9, float* P45, const float* acc, const float* q_wxyz, float dt, const float* pos_z,
+                     const uint8_t* pos_mask, const float* vel_z, const uint8_t* vel_mask, int32_t n, void* stream);
 int ouz_integrate(float* root13, const float* f_b, const float* tau_b, const float* mass, const float* inertia,
                   float dt, int32_t substeps, int32_t n, void* stream);
 int ouz_reward(const float* root13, const float* target, const int32_t* progress, int32_t max_episode_length,

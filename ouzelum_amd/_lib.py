@@ -112,6 +112,7 @@ SIGNATURES = {
     "ouz_pv_predict": (_I, [_P, _P, _P, _P, _F, _I, _P]),
     "ouz_pv_correct": (_I, [_P, _P, _P, _I, _F, _P, _I, _P]),
     "ouz_pv_step": (_I, [_P, _P, _P, _P, _F, _P, _P, _P, _P, _I, _P]),
+    "ouz_pv_step_quad": (_I, [_P, _P, _P, _P, _F, _P, _P, _P, _P, _I, _P]),
     "ouz_integrate": (_I, [_P, _P, _P, _P, _P, _F, _I, _I, _P]),
     "ouz_reward": (_I, [_P, _P, _P, _I, _F, _P, _P, _I, _P]),
     "ouz_philox": (_I, [_U64, _P, _U32, _U32, _U32, _P, _I, _P]),

@@ -21,7 +21,6 @@
 
 #include "../../include/ouzelum.h"
 #include "quad_math.h"
-#include "quad_pv_ql.h"
 
 #define OUZ_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
@@ -123,6 +122,10 @@ __device__ uint64_t g_ouz_stamps[kStampWaves * kStampSlots];
 #define OUZ_STAMP_RT(k) do {} while (0)
 constexpr int kStampSlots = 0;
 #endif
+#define OUZ_QL_STAMP(k) OUZ_STAMP(k, true)
+}  // namespace ouz
+#include "quad_pv_ql.h"
+namespace ouz {
 
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
 struct TaskParams {
@@ -187,6 +190,7 @@ struct StepArgs {
   int32_t track_episodes;
   int32_t pipe_stride;         // quad_step_pipe_kernel: waves in its grid (0: that kernel is not used)
   int32_t nt_loads;            // step kernels: non-temporal state loads (large N: nt_loads_default)
+  int32_t quad;                // trigger-class layout: the quad-lane estimator kernels (OUZ_QUAD_LANE=1; quad_pv_ql.h)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
@@ -738,10 +742,24 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
     if constexpr (QLN) {
-      // the covariance is in LDS and split over the env's lanes: no register peak to park around
+      // The covariance is in LDS and split over the env's lanes: no register peak to park around.  The values
+      // the one-lane form parks go through an empty asm instead, which seals them the way the LDS round trip
+      // does (the code on either side of the PV step is then contracted the same way in both forms, which
+      // keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
+      float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
+                        S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
+                        S.dr_m, S.dr_i, S.dr_t};
       pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u,
                  v3(vm[0], vm[1], vm[2]));
       OUZ_STAMP(12, false);
+#pragma unroll
+      for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
+      S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);
+      S.q = Q4{vals[9], vals[10], vals[11], vals[12]};
+      target = v3(vals[13], vals[14], vals[15]);
+      S.wp = v3(vals[16], vals[17], vals[18]);
+      S.plat = make_float2(vals[19], vals[20]);
+      S.dr_m = vals[21]; S.dr_i = vals[22]; S.dr_t = vals[23];
     } else {
       // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
       // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
@@ -975,7 +993,7 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
 __device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bool did_reset, int slot, int e) {
   if (a.trace_cap <= 0) return;
   const uint64_t m = __ballot(did_reset);
-  if ((slot & 63) == 0 && m) atomicAdd(&a.trace_resets[step % (uint32_t)a.trace_cap], (uint32_t)__popcll(m));
+  if ((threadIdx.x & 63u) == 0u && m) atomicAdd(&a.trace_resets[step % (uint32_t)a.trace_cap], (uint32_t)__popcll(m));
   if (e == 0) a.trace_resets[(step + 32u) % (uint32_t)a.trace_cap] = 0u;
 }
 
@@ -1210,7 +1228,7 @@ __host__ __device__ constexpr bool quad_lane_kernel(int task, bool cls) {
   return cls && (task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING || task == OUZ_TASK_MIXED);
 }
 
-template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false>
+template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QUAD = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
@@ -1218,7 +1236,7 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
-  if constexpr (quad_lane_kernel(TASK, CLS)) {
+  if constexpr (QUAD && quad_lane_kernel(TASK, CLS)) {
     // 64-lane blocks, four per tile: quarter q of tile t holds slots t*64 + q*16 .. +15, four lanes per slot
     const int tile = (int)(blockIdx.x >> 2), quarter = (int)(blockIdx.x & 3u);
     const int iq = tile * 64 + quarter * 16 + (int)(threadIdx.x >> 2);   // this quad's slot
@@ -1277,6 +1295,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     run_env<CTRL_RL, TGT_TRAJ, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
   } else if constexpr (TASK == OUZ_TASK_TRACKING) {
     run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, CLS, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, wrench);
+  } else if constexpr (CLS) {
+    // mixed curriculum, class layout: a wave's slots lie in one 1344-id chunk, so its task is wave-uniform
+    const uint32_t c = a.env_offset / kClassBlock + __builtin_amdgcn_readfirstlane((uint32_t)first) / kClassBlock;
+    const int t = mixed_chunk_task(c);
+    if (t == OUZ_TASK_LEE_LANDED)
+      run_env<CTRL_LEE_TRUE, TGT_PLATFORM, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                           OUZ_TASK_LEE_LANDED, false, sm, &ls, wrench);
+    else if (t == OUZ_TASK_TRACKING)
+      run_env<CTRL_LEE_EST, TGT_TRAJ, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                      OUZ_TASK_TRACKING, false, sm, &ls, wrench);
+    else
+      run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_FAULT,
+                                                 false, sm, &ls, wrench);
   } else {
     // Per-lane task; each task's lanes run in turn.  When the shard offset is a multiple of 64 the
     // curriculum's 64-env blocks coincide with waves and exactly one branch runs per wave.  Both
@@ -1295,31 +1326,31 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
       run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
                                         direct, sm, &ls, wrench);
   }
-  if (sm) reduce_stats(*rst, (uint32_t)first >> 6, (uint32_t)(a.n + 63) >> 6, ls);
+  if (sm) reduce_stats(*rst, (uint32_t)first >> 6, (uint32_t)((CLS ? a.n_slots : a.n) + 63) >> 6, ls);
 }
 
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
 // (~390 B): the host copies the argument block on every launch (≈0.6 us more host time per launch
 // for a 1.1 KB block, scripts/exp/launch_cost.hip), and at 4096 envs that host time is the bound.
-template <int TASK, bool CLS = false, bool NTL = false>
+template <int TASK, bool CLS = false, bool NTL = false, bool QUAD = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false, false, CLS, NTL>(a, &c, 1, env_out, 0);
+  step_body<TASK, false, false, CLS, NTL, QUAD>(a, &c, 1, env_out, 0);
 }
 
 // ouz_pre_physics: pre_physics_step alone, the body wrench to `wrench` [n][6].
-template <int TASK, bool CLS = false>
+template <int TASK, bool CLS = false, bool QUAD = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx c, float* wrench) {
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false, true, CLS>(a, &c, 1, env_out, 0, nullptr, wrench);
+  step_body<TASK, false, true, CLS, false, QUAD>(a, &c, 1, env_out, 0, nullptr, wrench);
 }
 
 // ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.
-template <int TASK, bool CLS = false>
+template <int TASK, bool CLS = false, bool QUAD = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true, false, CLS>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+  step_body<TASK, true, false, CLS, false, QUAD>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
@@ -1648,6 +1679,31 @@ __global__ void __launch_bounds__(64) pv_step_kernel(float* x, float* P, const f
   for (int k = 0; k < 45; ++k) P[i * 45 + k] = pp[k];
 }
 
+// The quad-lane form of pv_step_kernel (quad_pv_ql.h): 16 envs per 64-lane block, four lanes each.
+__global__ void __launch_bounds__(64) pv_step_quad_kernel(float* x, float* P, const float* acc, const float* q, float dt,
+                                                          const float* zp, const uint8_t* pmask, const float* zv,
+                                                          const uint8_t* vmask, int n) {
+  __shared__ double s_pv[16 * kPvLdsEnv];
+  const int i = blockIdx.x * 16 + (int)(threadIdx.x >> 2);
+  const uint32_t sub = threadIdx.x & 3u;
+  if (i >= n) return;   // whole quads only: the four lanes of an env share its fate
+  double* env_lds = s_pv + (threadIdx.x >> 2) * kPvLdsEnv;
+  const PvQl L{env_lds, env_lds + kPvLdsP, sub == 3u ? 0 : (int)sub, sub != 3u};
+  float xx[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) xx[k] = x[i * 9 + k];
+  pv_lds_load(L, [&](int f) { return P[i * 45 + f]; });
+  ql_sync();
+  pv_step_ql(L, xx, v3(acc[i * 3], acc[i * 3 + 1], acc[i * 3 + 2]), EkfQ{q[i * 4], q[i * 4 + 1], q[i * 4 + 2], q[i * 4 + 3]},
+             dt, pmask && pmask[i], zp ? v3(zp[i * 3], zp[i * 3 + 1], zp[i * 3 + 2]) : v3(0, 0, 0), vmask && vmask[i],
+             zv ? v3(zv[i * 3], zv[i * 3 + 1], zv[i * 3 + 2]) : v3(0, 0, 0));
+  if (sub == 0u) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k) x[i * 9 + k] = xx[k];
+  }
+  pv_lds_store(L, [&](int f, float v) { P[i * 45 + f] = v; });
+}
+
 __global__ void __launch_bounds__(64) integrate_kernel(float* root, const float* fb, const float* tb, const float* mass, const float* inertia,
                                  float dt, int substeps, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1898,6 +1954,12 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     if (a.cls) a.nt_loads = 0;   // the trigger-class layout (<= 64 K envs) has no such instantiation
   }
   {
+    // the quad-lane estimator kernels (quad_pv_ql.h): bit-identical results, opt-in -- measured slower than the
+    // one-lane kernels at 4096 envs (its LDS exchanges cost more than the f64 work they split)
+    const char* ql = std::getenv("OUZ_QUAD_LANE");
+    a.quad = (a.cls && ql && std::atoi(ql) != 0) ? 1 : 0;
+  }
+  {
     const char* rs = std::getenv("OUZ_ROLLOUT_STREAM");
     e->stream_rollout = rs ? std::atoi(rs) != 0 : stream_rollout_default(cfg->task, cfg->num_envs);
   }
@@ -2003,10 +2065,15 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
     }
   }
   if constexpr (class_layout_task(T)) {
-    if (a.cls) {   // the quad-lane grid: four 64-lane blocks per 64-slot tile (step_body)
+    if (a.cls && a.quad) {   // the quad-lane grid: four 64-lane blocks per 64-slot tile (step_body)
       const dim3 g4(g.x * 4);
-      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g4, b, 0, s, a, r.ctx[0]);
-      else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g4, b, 0, s, a, r);
+      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true, false, true>), g4, b, 0, s, a, r.ctx[0]);
+      else hipLaunchKernelGGL((quad_rollout_kernel<T, true, true>), g4, b, 0, s, a, r);
+      return;
+    }
+    if (a.cls) {
+      if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g, b, 0, s, a, r.ctx[0]);
+      else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g, b, 0, s, a, r);
       return;
     }
   }
@@ -2196,17 +2263,20 @@ int ouz_pre_physics(ouz_env* env, const float* actions, float* wrench, void* str
     case OUZ_TASK_OUZELUM: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_OUZELUM>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LEE_LANDED: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LEE_LANDED>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_EKF_LEE_LANDED:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true>), g4, b, 0, s, a, c, wrench);
+      if (a.cls && a.quad) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true, true>), g4, b, 0, s, a, c, wrench);
+      else if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, true>), g, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_EKF_LEE_LANDED, false>), g, b, 0, s, a, c, wrench);
       break;
     case OUZ_TASK_TRACKING:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true>), g4, b, 0, s, a, c, wrench);
+      if (a.cls && a.quad) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true, true>), g4, b, 0, s, a, c, wrench);
+      else if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, true>), g, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_TRACKING, false>), g, b, 0, s, a, c, wrench);
       break;
     case OUZ_TASK_FAULT: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_FAULT>, g, b, 0, s, a, c, wrench); break;
     case OUZ_TASK_LANDING: hipLaunchKernelGGL(quad_pre_kernel<OUZ_TASK_LANDING>, g, b, 0, s, a, c, wrench); break;
     default:
-      if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true>), g4, b, 0, s, a, c, wrench);
+      if (a.cls && a.quad) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true, true>), g4, b, 0, s, a, c, wrench);
+      else if (a.cls) hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, true>), g, b, 0, s, a, c, wrench);
       else hipLaunchKernelGGL((quad_pre_kernel<OUZ_TASK_MIXED, false>), g, b, 0, s, a, c, wrench);
       break;
   }
@@ -2350,6 +2420,17 @@ int ouz_pv_step(float* x, float* P, const float* acc, const float* q, float dt, 
   hipLaunchKernelGGL(pv_step_kernel, dim3(grid_for(n, 64)), dim3(64), 0, (hipStream_t)stream, x, P, acc, q, dt, pos_z,
                      pos_mask, vel_z, vel_mask, n);
   OUZ_LAUNCH_CHECK("pv_step_kernel");
+  return OUZ_OK;
+}
+
+int ouz_pv_step_quad(float* x, float* P, const float* acc, const float* q, float dt, const float* pos_z,
+                     const uint8_t* pos_mask, const float* vel_z, const uint8_t* vel_mask, int32_t n, void* stream) {
+  OUZ_CHECK_N("ouz_pv_step_quad");
+  if (!x || !P || !acc || !q) return fail(OUZ_ERR_INVALID, "ouz_pv_step_quad: null pointer");
+  if ((pos_mask && !pos_z) || (vel_mask && !vel_z)) return fail(OUZ_ERR_INVALID, "ouz_pv_step_quad: mask without data");
+  hipLaunchKernelGGL(pv_step_quad_kernel, dim3(grid_for(n, 16)), dim3(64), 0, (hipStream_t)stream, x, P, acc, q, dt,
+                     pos_z, pos_mask, vel_z, vel_mask, n);
+  OUZ_LAUNCH_CHECK("pv_step_quad_kernel");
   return OUZ_OK;
 }
 

@@ -10,23 +10,41 @@
 // exchange slot.  Every stored element is computed by the element formulas of quad_math.h (pvf_g0, pvf_g1,
 // pvf_z, dot3, dot3s, inv_sym3) on the same operands as the one-lane pv_step, so the two forms agree bit for
 // bit (the large-N kernels keep the one-lane form); like it, the step's results are rounded to f32 once, at
-// its end (`rnd` marks the last phase of the step: every correction rewrites all 45 stored elements, the
+// its end (RND marks the last phase of the step: every correction rewrites all 45 stored elements, the
 // predict all but the bias block, which it leaves unchanged).
+//
+// LDS traffic (measured, profiles/r03/): only the upper triangle of the 9x9 is written and every read addresses
+// an element by its upper position (row <= column), which halves the writes of a mirrored image; the per-env
+// stride of 131 doubles (262 dwords = 6 mod 64 banks) spreads the 16 envs x 3 columns of a wave over the banks
+// (the 108-double stride put envs 0 / 4 / 8 / 12 on one bank: ~45 cycles per ds_write_b64).
 #pragma once
 #include "quad_math.h"
 
+#ifndef OUZ_QL_STAMP
+#define OUZ_QL_STAMP(k) do {} while (0)   // instrumented builds (-DOUZ_STAMPS): sub-phase stamps
+#endif
+
 namespace ouz {
 
-constexpr int kPvLdsP = 81;                  // doubles of the full symmetric covariance
+constexpr int kPvLdsP = 81;                  // doubles of the 9x9 covariance (upper triangle used)
 constexpr int kPvLdsX = 27;                  // doubles of the exchange slot (three 3x3 matrices)
-constexpr int kPvLdsEnv = kPvLdsP + kPvLdsX; // per env
+constexpr int kPvLdsEnv = 131;               // per env, padded: 131 doubles = 262 dwords = 6 (mod 64 banks)
+static_assert(kPvLdsEnv >= kPvLdsP + kPvLdsX, "LDS image of one env");
 
 struct PvQl {
-  double* P;      // this env's 9x9 (row-major) in LDS
+  double* P;      // this env's 9x9 (row-major) in LDS; the upper triangle holds the covariance
   double* X;      // this env's exchange slot
   int c;          // this lane's block column (0..2)
   bool own;       // lanes 0..2 write; lane 3 computes lane 0's column and stays silent
 };
+// element k of column c of block (rb, bb), P[3 rb + k][3 bb + c], read at its upper position.  rb, bb and k
+// are compile-time after unrolling, so only a diagonal block's element below the diagonal (k > c) costs a
+// per-lane choice.
+__device__ __forceinline__ double qcol(const PvQl& L, int rb, int bb, int k) {
+  if (rb < bb) return L.P[(3 * rb + k) * 9 + 3 * bb + L.c];
+  if (rb > bb) return L.P[(3 * bb + L.c) * 9 + 3 * rb + k];
+  return k <= L.c ? L.P[(3 * rb + k) * 9 + 3 * bb + L.c] : L.P[(3 * bb + L.c) * 9 + 3 * rb + k];
+}
 
 // Wave-local LDS ordering: the wave's LDS accesses execute in program order; these keep the compiler from
 // moving them across an exchange (the same fence pair as the obs staging's wave_lds_sync).
@@ -36,21 +54,19 @@ __device__ __forceinline__ void ql_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ double rnd32(double v, bool rnd) { return rnd ? (double)(float)v : v; }
+template <bool RND>
+__device__ __forceinline__ double rnd32(double v) { return RND ? (double)(float)v : v; }
 
-// write element (r, k) of the symmetric P and its mirror
-__device__ __forceinline__ void ql_put(const PvQl& L, int r, int k, double v) {
-  L.P[r * 9 + k] = v;
-  L.P[k * 9 + r] = v;
-}
+// write element (r, k), r <= k, of the symmetric covariance (its upper position)
+__device__ __forceinline__ void ql_put(const PvQl& L, int r, int k, double v) { L.P[r * 9 + k] = v; }
 
 // one of three lane-indexed values: v[c] for this lane's c
 __device__ __forceinline__ double ql_sel(int c, double v0, double v1, double v2) {
   return c == 0 ? v0 : (c == 1 ? v1 : v2);
 }
 
-__device__ __forceinline__ void pv_predict_ql(const PvQl& L, double x[9], const double acc[3], EkfQ q, double dt,
-                                              bool rnd) {
+template <bool RND>
+__device__ __forceinline__ void pv_predict_ql(const PvQl& L, double x[9], const double acc[3], EkfQ q, double dt) {
   const M3T<double> M = pv_rot<double>(q);
   const double h = dt * dt * 0.5;
   pv_state_predict(x, acc, M, dt, h);
@@ -63,15 +79,16 @@ __device__ __forceinline__ void pv_predict_ql(const PvQl& L, double x[9], const 
     double X0[3], X1[3], X2[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      X0[k] = L.P[k * 9 + 3 * b + c];
-      X1[k] = L.P[(3 + k) * 9 + 3 * b + c];
-      X2[k] = L.P[(6 + k) * 9 + 3 * b + c];
+      X0[k] = qcol(L, 0, b, k);
+      X1[k] = qcol(L, 1, b, k);
+      X2[k] = qcol(L, 2, b, k);
     }
     pvf_g0(M, X0, X1, X2, dt, h, g0[b]);
     if (b > 0) pvf_g1(M, X1, X2, dt, g1[b - 1]);
   }
   double z00[3], z01[3], z11[3];
   pvf_z(g0[1], g0[2], g1[0], g1[1], dt, h, z00, z01, z11);
+  OUZ_QL_STAMP(14);
   // exchange the Z columns: X[m * 9 + col * 3 + row]
   if (L.own) {
 #pragma unroll
@@ -85,30 +102,33 @@ __device__ __forceinline__ void pv_predict_ql(const PvQl& L, double x[9], const 
   double Z[27];
 #pragma unroll
   for (int k = 0; k < 27; ++k) Z[k] = L.X[k];
+  OUZ_QL_STAMP(15);
   const double m0 = ql_sel(c, M.m[0], M.m[3], M.m[6]), m1 = ql_sel(c, M.m[1], M.m[4], M.m[7]),
                m2 = ql_sel(c, M.m[2], M.m[5], M.m[8]);   // row c of M
   double p00[3], p01[3], p11[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    p00[i] = rnd32(dot3s(Z[i], Z[3 + i], Z[6 + i], m0, m1, m2, i == c ? g0[0][i] + qhh : g0[0][i]), rnd);
-    p01[i] = rnd32(dot3s(Z[9 + i], Z[12 + i], Z[15 + i], m0, m1, m2, i == c ? qhd : 0.0), rnd);
-    p11[i] = rnd32(dot3s(Z[18 + i], Z[21 + i], Z[24 + i], m0, m1, m2, i == c ? qdd : 0.0), rnd);
+    p00[i] = rnd32<RND>(dot3s(Z[i], Z[3 + i], Z[6 + i], m0, m1, m2, i == c ? g0[0][i] + qhh : g0[0][i]));
+    p01[i] = rnd32<RND>(dot3s(Z[9 + i], Z[12 + i], Z[15 + i], m0, m1, m2, i == c ? qhd : 0.0));
+    p11[i] = rnd32<RND>(dot3s(Z[18 + i], Z[21 + i], Z[24 + i], m0, m1, m2, i == c ? qdd : 0.0));
   }
-  if (L.own) {   // the old P was read above (in-order LDS): overwrite it, mirrored
+  OUZ_QL_STAMP(16);
+  if (L.own) {   // the old P was read above (in-order LDS): overwrite its upper triangle
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i <= c) ql_put(L, i, c, p00[i]);
       ql_put(L, i, 3 + c, p01[i]);
       if (i <= c) ql_put(L, 3 + i, 3 + c, p11[i]);
-      ql_put(L, i, 6 + c, rnd32(g0[2][i], rnd));
-      ql_put(L, 3 + i, 6 + c, rnd32(g1[1][i], rnd));
+      ql_put(L, i, 6 + c, rnd32<RND>(g0[2][i]));
+      ql_put(L, 3 + i, 6 + c, rnd32<RND>(g1[1][i]));
     }
   }
   ql_sync();
+  OUZ_QL_STAMP(17);
 }
 
-template <int MB, bool R0>
-__device__ __forceinline__ void pv_correct_ql(const PvQl& L, double x[9], const double z[3], double r, bool rnd) {
+template <int MB, bool R0, bool RND>
+__device__ __forceinline__ void pv_correct_ql(const PvQl& L, double x[9], const double z[3], double r) {
   constexpr int A = (MB == 0) ? 1 : 0;
   constexpr int B = 2;
   const int c = L.c;
@@ -116,15 +136,15 @@ __device__ __forceinline__ void pv_correct_ql(const PvQl& L, double x[9], const 
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) S.m[i * 3 + j] = L.P[(3 * MB + i) * 9 + 3 * MB + j];
+    for (int j = i; j < 3; ++j) S.m[i * 3 + j] = S.m[j * 3 + i] = L.P[(3 * MB + i) * 9 + 3 * MB + j];
   S.m[0] += r; S.m[4] += r; S.m[8] += r;
   const M3T<double> Si = inv_sym3(S);
   // row c of K_A = P_{A,m} S^-1 and of K_B
   double ka[3], kb[3];
   {
-    const double* ra = L.P + (3 * A + c) * 9 + 3 * MB;
-    const double* rb = L.P + (3 * B + c) * 9 + 3 * MB;
-    const double a0 = ra[0], a1 = ra[1], a2 = ra[2], b0 = rb[0], b1 = rb[1], b2 = rb[2];
+    // row c of P_{A,m} and P_{B,m} = column c of P_{m,A} and P_{m,B}
+    const double a0 = qcol(L, MB, A, 0), a1 = qcol(L, MB, A, 1), a2 = qcol(L, MB, A, 2);
+    const double b0 = qcol(L, MB, B, 0), b1 = qcol(L, MB, B, 1), b2 = qcol(L, MB, B, 2);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       ka[j] = dot3(a0, a1, a2, Si.m[j], Si.m[3 + j], Si.m[6 + j]);
@@ -169,14 +189,13 @@ __device__ __forceinline__ void pv_correct_ql(const PvQl& L, double x[9], const 
   // column c of the other-other blocks
   double bb[3], ab[3], aa[3];
   {
-    const double pb0 = L.P[(3 * MB) * 9 + 6 + c], pb1 = L.P[(3 * MB + 1) * 9 + 6 + c], pb2 = L.P[(3 * MB + 2) * 9 + 6 + c];
-    const double pa0 = L.P[(3 * MB) * 9 + 3 * A + c], pa1 = L.P[(3 * MB + 1) * 9 + 3 * A + c],
-                 pa2 = L.P[(3 * MB + 2) * 9 + 3 * A + c];
+    const double pb0 = qcol(L, MB, B, 0), pb1 = qcol(L, MB, B, 1), pb2 = qcol(L, MB, B, 2);
+    const double pa0 = qcol(L, MB, A, 0), pa1 = qcol(L, MB, A, 1), pa2 = qcol(L, MB, A, 2);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      bb[i] = rnd32(dot3s(-KB[i][0], -KB[i][1], -KB[i][2], pb0, pb1, pb2, L.P[(6 + i) * 9 + 6 + c]), rnd);
-      ab[i] = rnd32(dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pb0, pb1, pb2, L.P[(3 * A + i) * 9 + 6 + c]), rnd);
-      aa[i] = rnd32(dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pa0, pa1, pa2, L.P[(3 * A + i) * 9 + 3 * A + c]), rnd);
+      bb[i] = rnd32<RND>(dot3s(-KB[i][0], -KB[i][1], -KB[i][2], pb0, pb1, pb2, qcol(L, B, B, i)));
+      ab[i] = rnd32<RND>(dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pb0, pb1, pb2, qcol(L, A, B, i)));
+      aa[i] = rnd32<RND>(dot3s(-KA[i][0], -KA[i][1], -KA[i][2], pa0, pa1, pa2, qcol(L, A, A, i)));
     }
   }
   // column c of the m-row blocks: MB < A: P_{m,A}[i][c] = r KA[c][i]; else P_{A,m}[i][c] = r KA[i][c];
@@ -188,9 +207,9 @@ __device__ __forceinline__ void pv_correct_ql(const PvQl& L, double x[9], const 
       ma[i] = mb[i] = mm[i] = 0.0;
     } else {
 #pragma clang fp contract(off)
-      ma[i] = rnd32(r * (MB < A ? ka[i] : ql_sel(c, KA[i][0], KA[i][1], KA[i][2])), rnd);
-      mb[i] = rnd32(r * kb[i], rnd);
-      mm[i] = rnd32(r * fma(-r, ql_sel(c, Si.m[i * 3], Si.m[i * 3 + 1], Si.m[i * 3 + 2]), i == c ? 1.0 : 0.0), rnd);
+      ma[i] = rnd32<RND>(r * (MB < A ? ka[i] : ql_sel(c, KA[i][0], KA[i][1], KA[i][2])));
+      mb[i] = rnd32<RND>(r * kb[i]);
+      mm[i] = rnd32<RND>(r * fma(-r, ql_sel(c, Si.m[i * 3], Si.m[i * 3 + 1], Si.m[i * 3 + 2]), i == c ? 1.0 : 0.0));
     }
   }
   if (L.own) {
@@ -214,20 +233,24 @@ __device__ __forceinline__ void pv_step_ql(const PvQl& L, float xf[9], V3 acc, E
 #pragma unroll
   for (int k = 0; k < 9; ++k) x[k] = (double)xf[k];
   const double a[3] = {(double)acc.x, (double)acc.y, (double)acc.z};
-  pv_predict_ql(L, x, a, q, (double)dt, !pos_fix && !vel_fix);
-  if (pos_fix) {
-    const double zz[3] = {(double)zp.x, (double)zp.y, (double)zp.z};
-    pv_correct_ql<0, false>(L, x, zz, (double)kPvPosVar, !vel_fix);
-  }
-  if (vel_fix) {
-    const double zz[3] = {(double)zv.x, (double)zv.y, (double)zv.z};
-    pv_correct_ql<1, true>(L, x, zz, 0.0, true);
+  // the trigger flags are wave-uniform under the trigger-class layout: one specialised body per case
+  const double zpd[3] = {(double)zp.x, (double)zp.y, (double)zp.z};
+  const double zvd[3] = {(double)zv.x, (double)zv.y, (double)zv.z};
+  if (!pos_fix && !vel_fix) {
+    pv_predict_ql<true>(L, x, a, q, (double)dt);
+  } else {
+    pv_predict_ql<false>(L, x, a, q, (double)dt);
+    if (pos_fix) {
+      if (vel_fix) pv_correct_ql<0, false, false>(L, x, zpd, (double)kPvPosVar);
+      else pv_correct_ql<0, false, true>(L, x, zpd, (double)kPvPosVar);
+    }
+    if (vel_fix) pv_correct_ql<1, true, true>(L, x, zvd, 0.0);
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k) xf[k] = (float)x[k];
 }
 
-// The covariance between HBM (packed upper f32, OUZ_F_PV_P) and LDS (full f64).  Lane c moves the packed
+// The covariance between HBM (packed upper f32, OUZ_F_PV_P) and LDS (upper triangle, f64).  Lane c moves the packed
 // elements it owns: column c of the upper blocks and the upper part (i <= c) of column c of the diagonal
 // blocks -- packed index s9(r, 3b + c) = g9(r) + 3b + c for r <= 3b + c, linear in c, so every access is the
 // lane's one offset (c fields further) plus an immediate.

@@ -54,3 +54,8 @@ if st[:, 12].any():
            ("ctrl: PV filter step", st[:, 12] - st[:, 11]), ("ctrl: guidance + Lee", st[:, 3] - st[:, 12])]
     for nm, v in sub:
         print(f"  {nm:24s} {np.median(v):8.0f} {np.percentile(v, 90):8.0f}")
+if st[:, 17].any():   # quad-lane PV sub-phases (quad_pv_ql.h OUZ_QL_STAMP 14-17)
+    for name, a, b in (("PV: X reads + G columns", 11, 14), ("PV: Z exchange", 14, 15), ("PV: P' columns", 15, 16),
+                       ("PV: P' writes", 16, 17), ("PV: after predict", 17, 12)):
+        dd = st[:, b] - st[:, a]
+        print(f"  {name:26s} {np.median(dd):6.0f} {np.percentile(dd, 90):8.0f}")

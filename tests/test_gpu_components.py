@@ -147,6 +147,44 @@ def test_pvfilter_sequence_vs_reference_golden(L, golden, seed, separate):
     assert err["P"] * ratio <= err["P32"], err
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_pv_step_quad_lane_matches_one_lane_bitwise(L, golden, seed):
+    """The quad-lane PV step of the latency-regime estimator kernels (ouz_pv_step_quad: four lanes per env, the
+    covariance in LDS, quad_pv_ql.h) against the one-lane form (ouz_pv_step): bit-identical state and packed
+    covariance over the adversarial golden sequence (28 chained steps, every trigger combination) and over 40
+    more steps on random inputs with the task's own trigger pattern (g % 7 == 6, g % 3 == 0), ragged n."""
+    g = golden("pvfilter.npz")
+    dt = float(g["dt"])
+    x0 = g[f"s{seed}_x0"]
+    n = x0.shape[0]
+    P0 = pack_sym(np.broadcast_to(np.eye(9) * Q.PV_P0, (n, 9, 9)), 9)
+    xa, Pa, xb, Pb = t(x0), t(P0), t(x0), t(P0)
+
+    def both(acc, qw, zp, tp, zv, tv, m):
+        for fn, x, P in ((L.lib.ouz_pv_step, xa, Pa), (L.lib.ouz_pv_step_quad, xb, Pb)):
+            L.check(fn(x.data_ptr(), P.data_ptr(), acc.data_ptr(), qw.data_ptr(), dt, zp.data_ptr(), tp.data_ptr(),
+                       zv.data_ptr(), tv.data_ptr(), m, stream()))
+        torch.cuda.synchronize()
+        assert torch.equal(xa, xb) and torch.equal(Pa, Pb)
+
+    for step in range(g[f"s{seed}_acc"].shape[0]):
+        both(t(g[f"s{seed}_acc"][step]), t(g[f"s{seed}_q_wxyz"][step]), t(g[f"s{seed}_pos"][step]),
+             t(g[f"s{seed}_trig_p"][step], torch.uint8), t(g[f"s{seed}_vel"][step]),
+             t(g[f"s{seed}_trig_v"][step], torch.uint8), n)
+    rs = np.random.RandomState(100 + seed)
+    m = 37                                   # ragged: the last quad block is partly idle
+    xa, xb = t(rs.normal(0, 1, (m, 9))), None
+    xb = xa.clone()
+    Pa = t(pack_sym(np.broadcast_to(np.eye(9) * Q.PV_P0, (m, 9, 9)), 9))
+    Pb = Pa.clone()
+    for k in range(40):
+        qv = rs.normal(0, 1, (m, 4))
+        qv[:, 0] += 3.0
+        gidx = k * m + np.arange(m)
+        both(t(rs.normal(0, 2, (m, 3))), t(qv / np.linalg.norm(qv, axis=1, keepdims=True)), t(rs.normal(0, 1, (m, 3))),
+             t(gidx % 7 == 6, torch.uint8), t(rs.normal(0, 1, (m, 3))), t(gidx % 3 == 0, torch.uint8), m)
+
+
 def test_integrate_vs_oracle(L):
     rs = np.random.RandomState(7)
     n = 1000

@@ -4,7 +4,11 @@ QuadTracking (config C) and EKFLeeLanded, 4096 envs, one whole episode (700 step
 with the task's own 300-step convergence window (:18; ekf_lee_landed.py:339,526-530), seeds {0, 1, 2}: the f32
 HIP env and the float64 oracle free-run from the same creation state and are compared every 50 steps.
 
-* reset_buf / time_outs / progress: exact, every env, every checkpoint.
+* reset_buf / time_outs / progress: exact for every env whose state never came within f32 round-off (1e-4) of a
+  done threshold (z_die 0.3 / distance 8, ekf_lee_landed.py:718) -- there an f32 and an f64 run may die one step
+  apart, as the single-step tests' near_threshold allows.  These are the drones whose DR thrust scale (U(0.9, 1.1),
+  config C) leaves the convergence window's fixed up-force 2.09 g below their weight: they sink slowly through the
+  z 0.3 line (QuadTracking: 21-27 of 4096 per seed come within 1e-4 of it); at most 1 % of the envs.
 * Positions and velocities of the envs that never came near one of the step's discrete decisions (landing cut
   0.25 m and waypoint-guidance switches 0.5 / 0.75 / 1.0 m, ekf_lee_landed.py:476-515; the deck contact and
   die lines; the husky's 0.2 m waypoint switch and 0.005 rad heading dead band, utils/controllers.py:27):
@@ -28,6 +32,7 @@ CLEAN_TOL = 1e-3      # m, DESIGN.md §4 (full-episode estimator free run)
 CLEAN_VTOL = 1e-2     # m/s
 ALL_TOL = 0.25        # m, the landing-cut radius (ekf_lee_landed.py:508)
 MARGIN = 1e-3         # an env within this of a decision threshold leaves the tight comparison for good
+DONE_MARGIN = 1e-4    # an env within this of a done threshold may legitimately die one step apart
 
 
 @pytest.fixture(scope="module")
@@ -47,18 +52,23 @@ def test_full_episode_estimator_free_run(ouz, task, seed):
     assert o.cfg.convergence_time == 300
     z = np.zeros((n, 4))
     margin = np.full(n, np.inf)
+    done_margin = np.full(n, np.inf)
     clean_counts, worst_clean = [], 0.0
     for k in range(steps):
         margin = np.fmin(margin, decision_margin(o, before=True))
         env.step(None)
         o.step(z)
         margin = np.fmin(margin, decision_margin(o, before=False))
+        d8 = np.sqrt(((o.target - o.p) ** 2).sum(-1))
+        done_margin = np.fmin(done_margin, np.minimum(np.abs(o.p[:, 2] - 0.3), np.abs(d8 - 8.0)))
         if (k + 1) % 50 == 0 or k + 1 == steps:
             g = gpu_snapshot(env)
             tag = f"{task} seed {seed} step {k + 1}"
-            np.testing.assert_array_equal(g["reset"], o.reset_buf, err_msg=tag)
-            np.testing.assert_array_equal(g["timeouts"], o.timeouts, err_msg=tag)
-            np.testing.assert_array_equal(g["progress"], o.progress, err_msg=tag)
+            exact = done_margin > DONE_MARGIN
+            assert (~exact).sum() <= n // 100, f"{tag}: {(~exact).sum()} envs near a done threshold"
+            np.testing.assert_array_equal(g["reset"][exact], o.reset_buf[exact], err_msg=tag)
+            np.testing.assert_array_equal(g["timeouts"][exact], o.timeouts[exact], err_msg=tag)
+            np.testing.assert_array_equal(g["progress"][exact], o.progress[exact], err_msg=tag)
             clean = margin > MARGIN
             clean_counts.append(int(clean.sum()))
             dp = np.abs(g["p"] - o.p).max(1)
@@ -71,4 +81,5 @@ def test_full_episode_estimator_free_run(ouz, task, seed):
     # the tight comparison covered the approach phase (f64 oracle, QuadTracking seed 0: 3206 / 1653 of 4096 envs
     # clean at steps 50 / 250; profiles/r03/estimator_free_run_sensitivity_oracle_f32_state.jsonl)
     assert clean_counts[0] >= 0.7 * n and clean_counts[5] >= 0.3 * n, f"too few envs in the tight comparison: {clean_counts}"
-    print(f"{task} seed {seed}: clean envs per checkpoint {clean_counts}, worst clean |dp| {worst_clean:.3g}")
+    print(f"{task} seed {seed}: clean envs per checkpoint {clean_counts}, worst clean |dp| {worst_clean:.3g}, "
+          f"{int((done_margin <= DONE_MARGIN).sum())} envs near a done threshold")
