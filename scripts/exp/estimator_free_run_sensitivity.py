@@ -36,7 +36,7 @@ def main():
     t0 = time.time()
     maxdev = np.zeros(n)
     margin = np.full(n, np.inf)
-    worst_clean = 0.0
+    worst_clean = worst_clean_v = 0.0
     for k in range(steps):
         margin = np.fmin(margin, decision_margin(a, before=True))
         a.step(z)
@@ -44,10 +44,12 @@ def main():
         round_state(b)
         margin = np.fmin(margin, decision_margin(a, before=False))
         d = np.abs(a.p - b.p).max(1)
+        dv = np.abs(a.v - b.v).max(1)
         maxdev = np.maximum(maxdev, d)
         clean = margin > 1e-3
         if clean.any():
             worst_clean = max(worst_clean, float(d[clean].max()))
+            worst_clean_v = max(worst_clean_v, float(dv[clean].max()))
         if (k + 1) % 50 == 0 or k + 1 == steps:
             rows.append({"step": k + 1, "max_dp": float(d.max()), "p99_dp": float(np.percentile(d, 99)),
                          "p999_dp": float(np.percentile(d, 99.9)), "median_dp": float(np.median(d)),
@@ -59,6 +61,7 @@ def main():
             print(json.dumps(rows[-1]), flush=True)
     print(json.dumps({"task": task, "n": n, "steps": steps, "seed": seed, "seconds": round(time.time() - t0, 1),
                       "max_dp_over_run": float(maxdev.max()), "worst_clean_dp": worst_clean,
+                      "worst_clean_dv": worst_clean_v,
                       "envs_max_dp_over_1e-3": int((maxdev > 1e-3).sum()),
                       "envs_max_dp_over_1e-2": int((maxdev > 1e-2).sum())}), flush=True)
 
