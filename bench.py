@@ -181,7 +181,8 @@ def load_traffic(kernel, task, n):
     rocprofv3 --stats average duration of the same workload), or None.  Summaries of another build are reported
     as stale, not used."""
     import glob
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_*_{kernel}_{task}_{n}_summary.json")))
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", f"pmc_*_{kernel}_{task}_{n}_summary.json"),
+                            recursive=True))
     if not hits:
         return None
     sha = loaded_lib_sha16()
@@ -204,7 +205,9 @@ def load_traffic(kernel, task, n):
                "source": os.path.relpath(h, ROOT), "lib_sha16": sha}
         if d.get("rocprof_avg_us"):
             out["rocprof_kernel_us_per_launch"] = round(d["rocprof_avg_us"], 3)
-            out["rocprof_stats"] = d.get("rocprof_stats_csv")
+            committed = h[:-len("_summary.json")] + "_kernel_stats.csv"   # the --stats CSV copied beside it
+            out["rocprof_stats"] = os.path.relpath(committed, ROOT) if os.path.exists(committed) \
+                else d.get("rocprof_stats_csv")
         return out
     return {"bytes_per_launch": None, "stale": f"no summary of library {sha}; newest of another build: {newest_other}"}
 

@@ -12,10 +12,11 @@ HIP env and the float64 oracle free-run from the same creation state and are com
 * Positions and velocities of the envs that never came near one of the step's discrete decisions (landing cut
   0.25 m and waypoint-guidance switches 0.5 / 0.75 / 1.0 m, ekf_lee_landed.py:476-515; the deck contact and
   die lines; the husky's 0.2 m waypoint switch and 0.005 rad heading dead band, utils/controllers.py:27):
-  |p_gpu - p_oracle| <= CLEAN_TOL.  CLEAN_TOL is derived in DESIGN.md §4 from the oracle's own sensitivity
-  (scripts/exp/estimator_free_run_sensitivity.py: the f64 oracle against a twin whose state is rounded to f32
-  after every step stays within 2.7e-5 m on such envs over the episode, p99.9 2e-5); the HIP step also rounds
-  its intermediates (f32 controller / integrator / EKF), hence the margin.
+  |p_gpu - p_oracle| <= CLEAN_TOL, |v_gpu - v_oracle| <= CLEAN_VTOL.  Both are derived in DESIGN.md §4 from the
+  oracle's own sensitivity (scripts/exp/estimator_free_run_sensitivity.py, seeds 0-2: the f64 oracle against a
+  twin whose state is rounded to f32 after every step stays within 2.8e-5 m / 5.1e-5 m/s (QuadTracking) and
+  1.9e-6 m / 3.1e-6 m/s (EKFLeeLanded) on such envs over the episode): 10x the position and 20x the velocity
+  figure, for the HIP step's f32 intermediates (controller / integrator / EKF), which the twin does not round.
 * Every env: |p_gpu - p_oracle| <= ALL_TOL, the landing-cut radius (an env whose cut / contact decision flips by
   one step lands a few centimetres from its twin and then rests on the deck with it).
 """
@@ -28,8 +29,8 @@ from tests.hip_helpers import decision_margin, gpu_snapshot
 
 pytestmark = pytest.mark.gpu
 
-CLEAN_TOL = 1e-3      # m, DESIGN.md §4 (full-episode estimator free run)
-CLEAN_VTOL = 1e-2     # m/s
+CLEAN_TOL = 3e-4      # m, DESIGN.md §4 (full-episode estimator free run)
+CLEAN_VTOL = 1e-3     # m/s
 ALL_TOL = 0.25        # m, the landing-cut radius (ekf_lee_landed.py:508)
 MARGIN = 1e-3         # an env within this of a decision threshold leaves the tight comparison for good
 DONE_MARGIN = 1e-4    # an env within this of a done threshold may legitimately die one step apart
