@@ -3,9 +3,9 @@
 // At 4096 envs an estimator wave is one dependent instruction chain on an otherwise idle CU, and the float64
 // PV covariance step is ~35 % of its instructions.  Here the four lanes of an env split that step: lane c
 // (c = lane & 3; lane 3 mirrors lane 0 and never writes) owns column c of every 3x3 block of the 9x9
-// covariance, so each lane evaluates a third of the block products.  The covariance lives in LDS as the full
-// symmetric 9x9 (f64) for the whole launch; every value a lane writes it writes to both mirrored positions, so
-// after a wave-local fence any lane reads any element in either orientation.  The 3x3 matrices whose full
+// covariance, so each lane evaluates a third of the block products.  The covariance lives in LDS as the upper
+// triangle of the symmetric 9x9 (f64) for the whole launch; after a wave-local fence any lane reads any element
+// through its upper position (qcol).  The 3x3 matrices whose full
 // rows every column needs (Z00 / Z01 / Z11 of the predict, the gains K of a correction) go through an LDS
 // exchange slot.  Every stored element is computed by the element formulas of quad_math.h (pvf_g0, pvf_g1,
 // pvf_z, dot3, dot3s, inv_sym3) on the same operands as the one-lane pv_step, so the two forms agree bit for
