@@ -234,6 +234,10 @@ int32_t ouz_abi_version(void);
 #define OUZ_BUILD_STAMPS 1u
 #define OUZ_BUILD_TEMPORAL_STORES 2u
 uint32_t ouz_build_flags(void);
+/* Waits of the split-wave estimator rollout (two waves per tile meeting in LDS) that gave up
+ * after ~70 ms instead of hanging the GPU, since the last reset: 0 unless the protocol is broken (its
+ * results are then wrong).  reset != 0 zeroes the counter after reading it.  Synchronous. */
+int ouz_split_timeouts(uint32_t* out, int32_t reset);
 /* State slots of a task at num_envs (see "State slots" above); negative on bad arguments. */
 int64_t ouz_state_slots(int32_t task, int32_t num_envs);
 /* State slot of each of num_envs envs of a shard starting at global id env_id_offset, into the host

@@ -85,6 +85,7 @@ _I64 = ctypes.c_int64
 SIGNATURES = {
     "ouz_abi_version": (_I, []),
     "ouz_build_flags": (_U32, []),
+    "ouz_split_timeouts": (_I, [_P, _I]),
     "ouz_state_slots": (_I64, [_I, _I]),
     "ouz_env_slots": (_I, [_I, _I, _I64, _P]),
     "ouz_last_error": (ctypes.c_char_p, []),

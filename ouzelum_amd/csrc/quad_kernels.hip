@@ -125,6 +125,7 @@ constexpr int kStampSlots = 0;
 #define OUZ_QL_STAMP(k) OUZ_STAMP(k, true)
 }  // namespace ouz
 #include "quad_pv_ql.h"
+#include "quad_pv_split.h"
 namespace ouz {
 
 // Task presets — mirror oracle/quad_oracle.py::task_spec.
@@ -191,6 +192,7 @@ struct StepArgs {
   int32_t pipe_stride;         // quad_step_pipe_kernel: waves in its grid (0: that kernel is not used)
   int32_t nt_loads;            // step kernels: non-temporal state loads (large N: nt_loads_default)
   int32_t quad;                // trigger-class layout: the quad-lane estimator kernels (OUZ_QUAD_LANE=1; quad_pv_ql.h)
+  int32_t split;               // trigger-class layout: the split-wave estimator rollout (OUZ_SPLIT_PV; quad_pv_split.h)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
@@ -609,10 +611,12 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
 // PRE: pre_physics_step only (ouz_pre_physics) -- stop before the integrator and write the body wrench
 // [6] (force, torque; body frame at the COM) that gym.simulate would integrate to `wrench`.
 // QLN: the quad-lane estimator (four lanes per env, the PV covariance in LDS at `ql`).
-template <int CTRL, int TGT, bool PRE = false, bool QLN = false>
+// SPW: the state wave of the split-wave estimator (quad_pv_split.h): the covariance is the other wave's.
+template <int CTRL, int TGT, bool PRE = false, bool QLN = false, bool SPW = false>
 __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
                                          EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout,
-                                         float* wrench = nullptr, const PvQl* ql = nullptr) {
+                                         float* wrench = nullptr, const PvQl* ql = nullptr,
+                                         const SplitLane* spl = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const EnvConsts& c = a.c;
   const bool rst = S.rst;
@@ -741,16 +745,20 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
-    if constexpr (QLN) {
-      // The covariance is in LDS and split over the env's lanes: no register peak to park around.  The values
-      // the one-lane form parks go through an empty asm instead, which seals them the way the LDS round trip
-      // does (the code on either side of the PV step is then contracted the same way in both forms, which
-      // keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
+    if constexpr (QLN || SPW) {
+      // The covariance is in LDS and split over the env's lanes (QLN) or in the other wave (SPW): no register
+      // peak to park around.  The values the one-lane form parks go through an empty asm instead, which seals
+      // them the way the LDS round trip does (the code on either side of the PV step is then contracted the
+      // same way in every form, which keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
       float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
                         S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
                         S.dr_m, S.dr_i, S.dr_t};
-      pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u,
-                 v3(vm[0], vm[1], vm[2]));
+      if constexpr (SPW)
+        pv_state_split(*spl, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
+                       g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
+      else
+        pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
+                   g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
       OUZ_STAMP(12, false);
 #pragma unroll
       for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
@@ -1010,17 +1018,22 @@ struct LaneStats {
 // the same env (same slot i and env e) and split its PV covariance step; every other part of the step runs
 // identically in all four, and lane 0 of the quad alone writes the env's outputs, statistics and state
 // (the lanes 0-2 write the covariance elements they own).
-template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QLN = false>
+// SPW: the state wave of the split-wave estimator rollout (quad_pv_split.h; MULTI only): the covariance is
+// stepped by the workgroup's other wave (cov_wave), the two meet in `spl_lds`.
+template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QLN = false,
+          bool SPW = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
                                         bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
-                                        float* wrench = nullptr) {
+                                        float* wrench = nullptr, SplitPvLds* spl_lds = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const uint32_t gid = a.env_offset + (uint32_t)e;
   // the env's outputs / statistics / state writes: every lane, or lane 0 of the quad
   const bool lead = QLN ? (threadIdx.x & 3u) == 0u : true;
   const bool vout = valid && lead;
   PvQl ql{};
+  SplitLane spl{spl_lds, 0, threadIdx.x & 63u};
+  static_assert(!SPW || (MULTI && !PRE && !QLN && CTRL == CTRL_LEE_EST), "the split form is the estimator rollout's");
   if constexpr (QLN) {
     static_assert(CTRL == CTRL_LEE_EST, "the quad-lane form is the estimator's");
     __shared__ double s_pv[16 * kPvLdsEnv];   // one 64-lane block = one wave = 16 envs
@@ -1032,7 +1045,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT, CLS, NTL, QLN>(a, e, tp, S, ctx[0].actions);
+  if (valid) env_load<CTRL, TGT, CLS, NTL, QLN || SPW>(a, e, tp, S, ctx[0].actions);
   if constexpr (QLN) {
     if (valid) pv_lds_load(ql, [&](int f) { return ld(S.T, OUZ_F_PV_P + f); });
     ql_sync();
@@ -1083,7 +1096,8 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       const bool did_reset = vout && S.rst;
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
       const bool flags_clear = vout && (k == 0 ? S.flags_clear : !did_reset);
-      if (valid) env_core<CTRL, TGT, false, QLN>(a, ctx[k], e, gid, task, S, ob, rew, rs, to, nullptr, &ql);
+      spl.k = k;
+      if (valid) env_core<CTRL, TGT, false, QLN, SPW>(a, ctx[k], e, gid, task, S, ob, rew, rs, to, nullptr, &ql, &spl);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT, CLS>(ctx[k + 1].actions, S, e);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i, e);
@@ -1131,7 +1145,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       S.ep_cnt_add = 0;   // env_store: no accumulator atomics
     }
   }
-  if (vout) env_store<CTRL, TGT, QLN>(a, i, tp, S);
+  if (vout) env_store<CTRL, TGT, QLN || SPW>(a, i, tp, S);
   if constexpr (QLN) {
     if (valid) pv_lds_store(ql, [&](int f, float v) { st(S.T, OUZ_F_PV_P + f, v); });
   }
@@ -1140,6 +1154,30 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
 }
 
 constexpr int kMaxRolloutChunk = 32;
+constexpr bool kSplitDefault = true;    // the split-wave estimator rollout is the default
+static_assert(kSplitRing >= kMaxRolloutChunk, "one attitude slot per step of a launch");
+
+// The covariance wave of the split-wave estimator rollout (quad_pv_split.h): the PV covariance of the tile's 64
+// envs through the K steps of the launch, loaded and stored once, stepped as the state wave publishes attitudes.
+__device__ __forceinline__ void cov_wave(const StepArgs& a, const StepCtx* ctx, int K, int i, int e, bool valid,
+                                         SplitPvLds& L) {
+  if (!__any(valid)) return;   // the state wave steps no env of this tile either
+  const Tile T = tile_of(a, i);
+  const uint32_t lane = threadIdx.x & 63u, gid = a.env_offset + (uint32_t)e;
+  float pf[45];
+#pragma unroll
+  for (int f = 0; f < 45; ++f) pf[f] = valid ? ld(T, OUZ_F_PV_P + f) : 0.0f;
+  for (int k = 0; k < K; ++k) {
+    // the fix decisions of env_core's PV step (g % 7 == 6 position, g % 3 == 0 velocity), for the lanes the
+    // state wave steps
+    const uint64_t g = (uint64_t)ctx[k].step * a.n_total + gid;
+    pv_cov_split(L, k, lane, pf, a.c.dt, valid && g % 7u == 6u, valid && g % 3u == 0u);
+  }
+  if (valid) {
+#pragma unroll
+    for (int f = 0; f < 45; ++f) st(T, OUZ_F_PV_P + f, pf[f]);
+  }
+}
 
 // Episode statistics fused into the last launch of a rollout (ouz_rollout_stats): each wave reduces its
 // lanes' totals into partials[wave]; the last wave to finish (device-scope ticket) adds the partials in
@@ -1228,7 +1266,8 @@ __host__ __device__ constexpr bool quad_lane_kernel(int task, bool cls) {
   return cls && (task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING || task == OUZ_TASK_MIXED);
 }
 
-template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QUAD = false>
+template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QUAD = false,
+          bool SPW = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
@@ -1236,6 +1275,48 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
+  if constexpr (SPW && quad_lane_kernel(TASK, CLS)) {
+    // The split-wave estimator rollout (quad_pv_split.h): 128-thread blocks, one per 64-slot tile; wave 0 steps
+    // the tile's envs, wave 1 their PV covariance.
+    static_assert(MULTI && !PRE && !QUAD, "the split form is the estimator rollout's");
+    __shared__ SplitPvLds s_split;
+    if (threadIdx.x == 0) {
+      s_split.att_count = 0;
+      s_split.gain_step[0] = 0;
+      s_split.gain_step[1] = 0;
+    }
+    __syncthreads();
+    const int tile = (int)blockIdx.x, i = tile * 64 + (int)(threadIdx.x & 63u);
+    int e;
+    int chunk_task = TASK;
+    if constexpr (TASK == OUZ_TASK_MIXED) {
+      const int64_t e64 = mixed_slot_env(a.env_offset, i);
+      e = (e64 >= 0 && e64 < a.n) ? (int)e64 : a.n;
+      chunk_task = mixed_chunk_task(a.env_offset / kClassBlock + (uint32_t)(tile * 64) / kClassBlock);
+    } else {
+      e = slot_env(i);
+    }
+    const bool valid = e < a.n;
+    constexpr int TGT = TASK == OUZ_TASK_EKF_LEE_LANDED ? TGT_PLATFORM : TGT_TRAJ;
+    if (threadIdx.x < 64u) {
+      if (chunk_task != OUZ_TASK_LEE_LANDED && chunk_task != OUZ_TASK_FAULT)
+        run_env<CTRL_LEE_EST, TGT, true, false, true, false, false, true>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK == OUZ_TASK_MIXED ? OUZ_TASK_TRACKING : TASK,
+            false, sm, &ls, nullptr, &s_split);
+      else if constexpr (TASK == OUZ_TASK_MIXED) {
+        if (chunk_task == OUZ_TASK_LEE_LANDED)
+          run_env<CTRL_LEE_TRUE, TGT_PLATFORM, true, false, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                                 OUZ_TASK_LEE_LANDED, false, sm, &ls);
+        else
+          run_env<CTRL_RL, TGT_GOAL, true, false, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
+                                                       OUZ_TASK_FAULT, false, sm, &ls);
+      }
+      if (sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // the state waves of the exact grid
+    } else if (chunk_task != OUZ_TASK_LEE_LANDED && chunk_task != OUZ_TASK_FAULT) {
+      cov_wave(a, ctx, K, i, e, valid, s_split);
+    }
+    return;
+  }
   if constexpr (QUAD && quad_lane_kernel(TASK, CLS)) {
     // 64-lane blocks, four per tile: quarter q of tile t holds slots t*64 + q*16 .. +15, four lanes per slot
     const int tile = (int)(blockIdx.x >> 2), quarter = (int)(blockIdx.x & 3u);
@@ -1346,11 +1427,12 @@ __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx
   step_body<TASK, false, true, CLS, false, QUAD>(a, &c, 1, env_out, 0, nullptr, wrench);
 }
 
-// ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.
-template <int TASK, bool CLS = false, bool QUAD = false>
+// ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.  SPW: the split-wave
+// estimator form (quad_pv_split.h), 128-thread blocks.
+template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true, false, CLS, false, QUAD>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+  step_body<TASK, true, false, CLS, false, QUAD, SPW>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
@@ -1804,6 +1886,16 @@ struct ouz_env {
 
 extern "C" {
 
+int ouz_split_timeouts(uint32_t* out, int32_t reset) {
+  if (!out) return fail(OUZ_ERR_INVALID, "ouz_split_timeouts: null pointer");
+  int r = hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ouz_split_timeouts), sizeof(uint32_t)),
+                    "hipMemcpyFromSymbol(split timeouts)");
+  if (r || !reset) return r;
+  const uint32_t zero = 0;
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_ouz_split_timeouts), &zero, sizeof(uint32_t)),
+                   "hipMemcpyToSymbol(split timeouts)");
+}
+
 #ifdef OUZ_STAMPS
 int ouz_probe_stamps(uint64_t* host, int32_t count) {
   const int n = count < kStampWaves * kStampSlots ? count : kStampWaves * kStampSlots;
@@ -1958,6 +2050,9 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     // one-lane kernels at 4096 envs (its LDS exchanges cost more than the f64 work they split)
     const char* ql = std::getenv("OUZ_QUAD_LANE");
     a.quad = (a.cls && ql && std::atoi(ql) != 0) ? 1 : 0;
+    // the split-wave estimator rollout (quad_pv_split.h): bit-identical results; OUZ_SPLIT_PV=0 / 1 overrides
+    const char* sp = std::getenv("OUZ_SPLIT_PV");
+    a.split = (a.cls && !a.quad && (sp ? std::atoi(sp) != 0 : kSplitDefault)) ? 1 : 0;
   }
   {
     const char* rs = std::getenv("OUZ_ROLLOUT_STREAM");
@@ -2069,6 +2164,10 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
       const dim3 g4(g.x * 4);
       if (single) hipLaunchKernelGGL((quad_step_kernel<T, true, false, true>), g4, b, 0, s, a, r.ctx[0]);
       else hipLaunchKernelGGL((quad_rollout_kernel<T, true, true>), g4, b, 0, s, a, r);
+      return;
+    }
+    if (a.cls && a.split && !single) {   // the split-wave estimator rollout: two waves per 64-slot tile
+      hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, true>), g, dim3(128), 0, s, a, r);
       return;
     }
     if (a.cls) {

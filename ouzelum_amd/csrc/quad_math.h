@@ -497,11 +497,10 @@ OUZ_HD void pvf_z(const T g01[3], const T g02[3], const T g11[3], const T g12[3]
   }
 }
 
+// prediction_step, covariance part only (the split form's covariance wave: quad_kernels.hip SplitPv)
 template <typename T>
-OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
-  const M3T<T> M = pv_rot<T>(q);
+OUZ_HD void pv_cov_predict_t(T P[45], const M3T<T>& M, T dt) {
   const T h = dt * dt * T(0.5);
-  pv_state_predict(x, acc, M, dt, h);
   const T q_a = (T)kPvAccVar, qhh = q_a * h * h, qhd = q_a * h * dt, qdd = q_a * dt * dt;
   // every G column from the old P before anything is written: g[b][c][i] = G_{0,b}[i][c], g1[b-1][c][i] = G_{1,b}
   T g0[3][3][3], g1[2][3][3];
@@ -536,6 +535,14 @@ OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
   }
 }
 
+template <typename T>
+OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
+  const M3T<T> M = pv_rot<T>(q);
+  const T h = dt * dt * T(0.5);
+  pv_state_predict(x, acc, M, dt, h);
+  pv_cov_predict_t(P, M, dt);
+}
+
 // correction_step for one measured block m (0 = position, 1 = velocity) with R = r I.
 // Stable form of x += K (z - x_m); P = (I - K H) P  (DESIGN.md §4), the other blocks A < B:
 //   S = P_mm + r I;  K_o = P_om S^-1;  x_m = z - r S^-1 y;  x_o += K_o y   (y = z - x_m)
@@ -544,8 +551,10 @@ OUZ_HD void pv_predict_t(T x[9], T P[45], const T acc[3], EkfQ q, T dt) {
 // P_mm = P_mo = 0, written as zeros (IEEE f64 cannot fold 0 * x).
 // Row i of K_o = row i of P_om times S^-1; element (i, c) of an updated block = seed - (row i of K) . (column c
 // of P_mo); the quad-lane form computes row c of each K and column c of each block.
-template <int MB, typename T, bool R0 = false>
-OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
+// The correction in three parts, each element by the same formula wherever it is evaluated: the gains from
+// the covariance, the state update from the gains, the covariance update from the gains.
+template <int MB, typename T>
+OUZ_HD void pv_gain_t(const T P[45], T r, M3T<T>& Si, T KA[3][3], T KB[3][3]) {
 #pragma clang fp contract(off)
   constexpr int A = (MB == 0) ? 1 : 0;   // the two other blocks, A < B
   constexpr int B = 2;
@@ -555,8 +564,7 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) S.m[i * 3 + j] = P[s9(3 * MB + i, 3 * MB + j)];
   S.m[0] += r; S.m[4] += r; S.m[8] += r;
-  const M3T<T> Si = inv_sym3(S);
-  T KA[3][3], KB[3][3];
+  Si = inv_sym3(S);
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -566,24 +574,36 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
       KB[i][j] = dot3(P[s9(3 * B + i, 3 * MB)], P[s9(3 * B + i, 3 * MB + 1)], P[s9(3 * B + i, 3 * MB + 2)],
                       Si.m[j], Si.m[3 + j], Si.m[6 + j]);
     }
-  {
-    T y[3];
+}
+
+template <int MB, typename T, bool R0 = false>
+OUZ_HD void pv_x_correct_t(T x[9], const T z[3], T r, const M3T<T>& Si, const T KA[3][3], const T KB[3][3]) {
+#pragma clang fp contract(off)
+  constexpr int A = (MB == 0) ? 1 : 0;
+  constexpr int B = 2;
+  T y[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) y[k] = z[k] - x[MB * 3 + k];
-    T xm[3], dA[3], dB[3];
+  for (int k = 0; k < 3; ++k) y[k] = z[k] - x[MB * 3 + k];
+  T xm[3], dA[3], dB[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      xm[i] = R0 ? z[i] : fma(-r, dot3(Si.m[i * 3], Si.m[i * 3 + 1], Si.m[i * 3 + 2], y[0], y[1], y[2]), z[i]);
-      dA[i] = dot3(KA[i][0], KA[i][1], KA[i][2], y[0], y[1], y[2]);
-      dB[i] = dot3(KB[i][0], KB[i][1], KB[i][2], y[0], y[1], y[2]);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      x[MB * 3 + k] = xm[k];
-      x[A * 3 + k] += dA[k];
-      x[B * 3 + k] += dB[k];
-    }
+  for (int i = 0; i < 3; ++i) {
+    xm[i] = R0 ? z[i] : fma(-r, dot3(Si.m[i * 3], Si.m[i * 3 + 1], Si.m[i * 3 + 2], y[0], y[1], y[2]), z[i]);
+    dA[i] = dot3(KA[i][0], KA[i][1], KA[i][2], y[0], y[1], y[2]);
+    dB[i] = dot3(KB[i][0], KB[i][1], KB[i][2], y[0], y[1], y[2]);
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    x[MB * 3 + k] = xm[k];
+    x[A * 3 + k] += dA[k];
+    x[B * 3 + k] += dB[k];
+  }
+}
+
+template <int MB, typename T, bool R0 = false>
+OUZ_HD void pv_cov_correct_t(T P[45], T r, const M3T<T>& Si, const T KA[3][3], const T KB[3][3]) {
+#pragma clang fp contract(off)
+  constexpr int A = (MB == 0) ? 1 : 0;
+  constexpr int B = 2;
   // the other-other blocks first: they read the m-row blocks, which are overwritten below
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -617,6 +637,15 @@ OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
         if (i <= c) P[s9(3 * MB + i, 3 * MB + c)] = r * fma(-r, Si.m[i * 3 + c], i == c ? T(1) : T(0));
       }
     }
+}
+
+template <int MB, typename T, bool R0 = false>
+OUZ_HD void pv_correct_t(T x[9], T P[45], const T z[3], T r) {
+  M3T<T> Si;
+  T KA[3][3], KB[3][3];
+  pv_gain_t<MB, T>(P, r, Si, KA, KB);
+  pv_x_correct_t<MB, T, R0>(x, z, r, Si, KA, KB);
+  pv_cov_correct_t<MB, T, R0>(P, r, Si, KA, KB);
 }
 
 // One PV-filter step as the driver runs it (ekf_lee_landed.py:417-444): predict, then the

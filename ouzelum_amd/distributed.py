@@ -45,48 +45,48 @@ def allreduce_returns(stats):
     return s / c if c > 0 else float("nan")
 
 
-class GraphCollectives:
-    """The row-range all-reduces of a ``ReturnAllReduce`` slot block, captured once as hipGraphs and launched
-    through raw HIP calls on a collective stream of their own.
+class DirectCollectives:
+    """The flushes of a ``ReturnAllReduce`` slot block as direct RCCL calls on the communicator the process
+    group already holds, on a collective stream of their own.
 
-    An eager ``dist.all_reduce(async_op=True)`` costs 14-22 us of host time (ProcessGroupNCCL's work object,
-    events and stream bookkeeping around the RCCL call; measured on a one-rank group, where RCCL itself does
-    nothing for an in-place reduction: ``profiles/r03/allreduce_graph.jsonl``).  Every flush of a block is a
-    fixed row range [lo, hi) of a fixed buffer, so all of them can be captured at construction (depth x
-    batch (batch + 1) / 2 graphs, ~0.05 ms of capture each); a flush then costs four HIP calls -- record
-    an event on the caller's stream, make the collective stream wait for it, ``hipGraphLaunch``, record the
-    graph's completion event -- and a wait one ``hipStreamWaitEvent``.  RCCL supports stream capture;
-    every rank replays the same graphs in the same order, exactly as it would call the collectives.
+    Host cost of one flush (``scripts/exp/allreduce_graph.py``, ``profiles/r03/allreduce_host.jsonl``, medians of
+    per-call times on two boxes): ``dist.all_reduce(async_op=True)`` 13-20 us (ProcessGroupNCCL's work object,
+    events and stream bookkeeping); the collective captured in a hipGraph and replayed behind an event pair
+    12-14 us (``hipGraphLaunch`` of a one-kernel graph alone is 7-9 us on this ROCm); this form behind the
+    event pair 7-12 us (each ``hipEventRecord`` 1.7-2.3 us); this form in the caller's stream 1.2 us (one
+    rank: RCCL enqueues nothing) to 4.5 us (with one device operation enqueued, the stand-in for the RCCL
+    kernel of a multi-rank call).  The asynchronous flush of a full block (``submit``) goes behind the event
+    pair on the collective stream, so the next rollouts step while it runs; a flush the caller waits for
+    next (``finish``, ``result``) goes in the caller's stream.  Every rank makes the same calls in the same
+    order, exactly as it would call ``dist.all_reduce``; RCCL runs a communicator's operations in that order
+    whatever stream they are on.
     """
 
-    LIB = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    LIB = os.path.join(os.path.dirname(torch.__file__), "lib")
+    NCCL_FLOAT64, NCCL_SUM = 8, 0
 
     def __init__(self, slots):
         import ctypes
         self._ct = ctypes
-        self.hip = ctypes.CDLL(self.LIB)
+        self.hip = ctypes.CDLL(os.path.join(self.LIB, "libamdhip64.so"))
+        self.rccl = ctypes.CDLL(os.path.join(self.LIB, "librccl.so"))
+        self.rccl.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        self.rccl.ncclAllReduce.restype = ctypes.c_int
         dev = slots.device
+        self._dev = dev
         self.cs = torch.cuda.Stream(device=dev)
         self._cs = ctypes.c_void_p(self.cs.cuda_stream)
-        self._dev = dev
-        depth, batch = slots.shape[0], slots.shape[1]
-        cur = torch.cuda.current_stream(dev)
-        self.cs.wait_stream(cur)
-        with torch.cuda.stream(self.cs):
-            dist.all_reduce(slots[0, :1], op=dist.ReduceOp.SUM)   # communicator set up outside the capture
-            self.graphs = {}
-            for d in range(depth):
-                for lo in range(batch):
-                    for hi in range(lo + 1, batch + 1):
-                        g = torch.cuda.CUDAGraph()
-                        g.capture_begin(capture_error_mode="thread_local")
-                        try:
-                            dist.all_reduce(slots[d, lo:hi], op=dist.ReduceOp.SUM)
-                        finally:
-                            g.capture_end()
-                        self.graphs[(d, lo, hi)] = (g, ctypes.c_void_p(g.raw_cuda_graph_exec()), self._event())
-        cur.wait_stream(self.cs)
+        pg = dist.distributed_c10d._get_default_group()._get_backend(dev)
+        comm = pg._comm_ptr()
+        if not comm:
+            raise RuntimeError("the process group has no RCCL communicator")
+        self._comm = ctypes.c_void_p(comm)
+        self._base = slots.data_ptr()
+        self._width = slots.shape[2]
+        self._batch = slots.shape[1]
         self._ev_in = self._event()
+        self._done = [[self._event() for _ in range(slots.shape[1])] for _ in range(slots.shape[0])]
 
     def _event(self):
         e = self._ct.c_void_p()
@@ -94,19 +94,27 @@ class GraphCollectives:
             raise RuntimeError("hipEventCreateWithFlags failed")
         return e
 
-    def _check(self, err, what):
+    @staticmethod
+    def _check(err, what):
         if err != 0:
-            raise RuntimeError(f"{what} failed (hipError {err})")
+            raise RuntimeError(f"{what} failed (error {err})")
 
-    def launch(self, d, lo, hi):
-        """Reduce rows [lo, hi) of block d after the work queued so far on the caller's stream; returns the
-        completion event."""
+    def launch(self, d, lo, hi, in_stream=False):
+        """Sum rows [lo, hi) of block d over the ranks, after the work queued so far on the caller's stream;
+        returns the completion event.  in_stream: on the caller's stream itself (for a caller about to wait
+        for the result anyway: one RCCL call, no event pair); returns None."""
         from . import _lib
-        _, ex, done = self.graphs[(d, lo, hi)]
+        done = self._done[d][lo]
         s = self._ct.c_void_p(_lib.stream_ptr(self._dev))
+        p = self._ct.c_void_p(self._base + ((d * self._batch + lo) * self._width) * 8)
+        if in_stream:
+            self._check(self.rccl.ncclAllReduce(p, p, (hi - lo) * self._width, self.NCCL_FLOAT64, self.NCCL_SUM,
+                                                self._comm, s), "ncclAllReduce")
+            return None
         self._check(self.hip.hipEventRecord(self._ev_in, s), "hipEventRecord")
         self._check(self.hip.hipStreamWaitEvent(self._cs, self._ev_in, 0), "hipStreamWaitEvent")
-        self._check(self.hip.hipGraphLaunch(ex, self._cs), "hipGraphLaunch")
+        self._check(self.rccl.ncclAllReduce(p, p, (hi - lo) * self._width, self.NCCL_FLOAT64, self.NCCL_SUM,
+                                            self._comm, self._cs), "ncclAllReduce")
         self._check(self.hip.hipEventRecord(done, self._cs), "hipEventRecord")
         return done
 
@@ -120,8 +128,9 @@ class GraphCollectives:
         hip = getattr(self, "hip", None)
         if hip is None:
             return
-        for _, _, e in getattr(self, "graphs", {}).values():
-            hip.hipEventDestroy(e)
+        for row in getattr(self, "_done", []):
+            for e in row:
+                hip.hipEventDestroy(e)
         if getattr(self, "_ev_in", None):
             hip.hipEventDestroy(self._ev_in)
 
@@ -135,11 +144,11 @@ class ReturnAllReduce:
     helper keeps ``depth`` blocks of ``batch`` stat rows: rollout r's stats go to row r % batch of
     block (r // batch) % depth, and a block is all-reduced asynchronously, in ONE collective, once
     its last row is submitted, on the collective's own stream while the next rollouts step.  One
-    eager call of ``dist.all_reduce`` costs 14-22 us of host time (RCCL, ``profiles/r01/allreduce_host.txt``,
-    ``profiles/r03/allreduce_graph.jsonl``), as much as five 4096-env steps, so ``batch`` rollouts
-    share it; the per-rollout global statistics are unchanged.  ``collective="graph"`` (the default on
-    the "nccl" backend, i.e. RCCL) replays pre-captured hipGraphs of the same collectives instead
-    (``GraphCollectives``, a few us of host time per flush); it is checked against the eager form at
+    eager call of ``dist.all_reduce`` costs 13-22 us of host time (RCCL, ``profiles/r01/allreduce_host.txt``,
+    ``profiles/r03/allreduce_host.jsonl``), as much as five 4096-env steps, so ``batch`` rollouts
+    share it; the per-rollout global statistics are unchanged.  ``collective="direct"`` (the default on
+    the "nccl" backend, i.e. RCCL) issues the same collectives as direct RCCL calls on the process group's
+    communicator instead (``DirectCollectives``, about half the host time per flush); it is checked at
     construction on every rank and falls back to eager, on all ranks together, if the check fails.
     ``OUZ_COLLECTIVE=eager`` forces the eager form.  A block is only reused after its
     collectives have completed (``wait`` orders the current stream after them).  ``result(r)``
@@ -158,18 +167,18 @@ class ReturnAllReduce:
         self.active = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
         self._base = None
         self._row_bytes = width * self.slots.element_size()
-        self.graphs = None
+        self.direct = None
         if collective is None:
-            collective = os.environ.get("OUZ_COLLECTIVE", "graph")
-        if collective not in ("graph", "eager"):
-            raise ValueError(f"collective must be 'graph' or 'eager', not {collective!r}")
-        if (self.active and collective == "graph" and self.slots.is_cuda
+            collective = os.environ.get("OUZ_COLLECTIVE", "direct")
+        if collective not in ("direct", "eager"):
+            raise ValueError(f"collective must be 'direct' or 'eager', not {collective!r}")
+        if (self.active and collective == "direct" and self.slots.is_cuda
                 and dist.get_backend() == dist.Backend.NCCL):
-            self.graphs = self._graph_collectives()
-        self.collective = "graph" if self.graphs is not None else "eager"
+            self.direct = self._direct_collectives()
+        self.collective = "direct" if self.direct is not None else "eager"
 
-    def _graph_collectives(self):
-        """Capture the block collectives and check them once against the known sums; every rank takes the
+    def _direct_collectives(self):
+        """Set up the direct collectives and check them once against the known sums; every rank takes the
         same decision (an eager all-reduce of the verdicts)."""
         rank, world = dist.get_rank(), dist.get_world_size()
 
@@ -178,11 +187,13 @@ class ReturnAllReduce:
             dist.all_reduce(v, op=dist.ReduceOp.MIN)
             return v.item() == 1.0
 
+        dist.all_reduce(self.slots[0, :1], op=dist.ReduceOp.SUM)   # every rank: the communicator exists
+        torch.cuda.synchronize(self.slots.device)
         try:
-            g = GraphCollectives(self.slots)
-        except Exception:   # noqa: BLE001 -- a capture failure means: use the eager collectives
+            g = DirectCollectives(self.slots)
+        except Exception:   # noqa: BLE001 -- a setup failure means: use the eager collectives
             g = None
-        if not agree(g is not None):   # captured graphs run no collective: the ranks are still in step here
+        if not agree(g is not None):   # the setup runs no collective: the ranks are still in step here
             return None
         ok = True
         try:
@@ -208,16 +219,22 @@ class ReturnAllReduce:
 
     def _wait(self, d):
         for w in self.works[d]:
-            if self.graphs is not None:
-                self.graphs.wait(w)
+            if self.direct is not None:
+                self.direct.wait(w)
             else:
                 w.wait()
         self.works[d] = []
 
-    def _flush(self, d, hi):
+    def _flush(self, d, hi, now=False):
+        """now: the caller waits for these rows next (finish / result), so the direct form reduces them in its
+        stream (one RCCL call, ~1-5 us of host time) instead of on the collective stream behind an event pair."""
         if self.active and self.lo[d] < hi:
-            if self.graphs is not None:
-                self.works[d].append(self.graphs.launch(d, self.lo[d], hi))
+            if self.direct is not None:
+                if now:
+                    self._wait(d)   # the block's earlier rows first: the calls stay in the same order everywhere
+                    self.direct.launch(d, self.lo[d], hi, in_stream=True)
+                else:
+                    self.works[d].append(self.direct.launch(d, self.lo[d], hi))
             else:
                 self.works[d].append(dist.all_reduce(self.slots[d, self.lo[d]:hi], op=dist.ReduceOp.SUM,
                                                      async_op=True))
@@ -257,11 +274,11 @@ class ReturnAllReduce:
         if not self.active:
             return
         for d in range(self.depth):
-            self._flush(d, self.filled[d])
+            self._flush(d, self.filled[d], now=True)
             self._wait(d)
 
     def result(self, r):
         d, row = self._where(r)
-        self._flush(d, row + 1)
+        self._flush(d, row + 1, now=True)
         self._wait(d)
         return self.slots[d, row]

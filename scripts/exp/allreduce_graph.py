@@ -2,10 +2,12 @@
 "nccl" (RCCL) group on one GPU; the tensor is a ReturnAllReduce block ([batch, 3] float64):
 
 * eager     -- ``dist.all_reduce(async_op=True)`` (ProcessGroupNCCL: work object, events, stream bookkeeping);
-* graph     -- GraphCollectives: record an event on the caller's stream, wait for it on the collective stream,
-               ``hipGraphLaunch`` of the pre-captured collective, record its completion event;
-* direct    -- the same event pair around one ``ncclAllReduce`` call through ctypes on torch's librccl, on the
-               communicator ProcessGroupNCCL already holds (``_comm_ptr``).
+* graph     -- record an event on the caller's stream, wait for it on a collective stream, ``hipGraphLaunch`` of
+               the collective captured once, record its completion event;
+* direct    -- ouzelum_amd.distributed.DirectCollectives (ReturnAllReduce's default on RCCL): the same event pair
+               around one ``ncclAllReduce`` call through ctypes on torch's librccl, on the communicator
+               ProcessGroupNCCL already holds (``_comm_ptr``); "in stream": the RCCL call alone, on the
+               caller's stream (no events; the next rollouts would then wait for the collective).
 
 A one-rank in-place RCCL all-reduce enqueues no GPU work (RCCL returns at once for one rank), so the captured
 graph is empty; the "kernel" variants stand in for what a multi-rank call enqueues: a graph holding one kernel
@@ -27,7 +29,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from ouzelum_amd import _lib  # noqa: E402
-from ouzelum_amd.distributed import GraphCollectives  # noqa: E402
+from ouzelum_amd.distributed import DirectCollectives  # noqa: E402
 
 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29541")
@@ -35,7 +37,6 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
 hip = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
-rccl = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
 NCCL_FLOAT64, NCCL_SUM = 8, 0
 
 
@@ -73,50 +74,55 @@ for batch in [int(a) for a in sys.argv[1:]] or [1, 8]:
     for w in works:
         w.wait()
 
-    g = GraphCollectives(slots)
-    torch.cuda.synchronize()
-    res["graph_us"] = per_call_us(lambda: g.launch(0, 0, batch))
-    proxy = torch.cuda.CUDAGraph()
-    g.cs.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(g.cs):
-        proxy.capture_begin(capture_error_mode="thread_local")
-        blk.mul_(1.0)
-        proxy.capture_end()
-    torch.cuda.synchronize()
-    g.graphs[(0, 0, batch)] = (proxy, ctypes.c_void_p(proxy.raw_cuda_graph_exec()), g.graphs[(0, 0, batch)][2])
-    res["graph_kernel_node_us"] = per_call_us(lambda: g.launch(0, 0, batch))
-
-    # direct RCCL call on the process group's communicator
-    pg = dist.distributed_c10d._get_default_group()._get_backend(dev)
-    comm = ctypes.c_void_p(pg._comm_ptr())
-    cs = ctypes.c_void_p(g.cs.cuda_stream)
+    cs_t = torch.cuda.Stream(device=dev)
+    cs = ctypes.c_void_p(cs_t.cuda_stream)
     ev_in, ev_done = event(), event()
 
-    def direct(send, recv):
+    def graph_flush(ex):
         s = ctypes.c_void_p(_lib.stream_ptr(dev))
         assert hip.hipEventRecord(ev_in, s) == 0
         assert hip.hipStreamWaitEvent(cs, ev_in, 0) == 0
-        err = rccl.ncclAllReduce(ctypes.c_void_p(send), ctypes.c_void_p(recv), ctypes.c_size_t(batch * 3),
-                                 NCCL_FLOAT64, NCCL_SUM, comm, cs)
-        assert err == 0, err
+        assert hip.hipGraphLaunch(ex, cs) == 0
         assert hip.hipEventRecord(ev_done, cs) == 0
 
-    res["direct_us"] = per_call_us(lambda: direct(blk.data_ptr(), blk.data_ptr()))
-    res["direct_out_of_place_us"] = per_call_us(lambda: direct(other.data_ptr(), blk.data_ptr()))
+    graphs = []
+    for body in (lambda: dist.all_reduce(blk, op=dist.ReduceOp.SUM), lambda: blk.mul_(1.0)):
+        gr = torch.cuda.CUDAGraph()
+        cs_t.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs_t):
+            gr.capture_begin(capture_error_mode="thread_local")
+            body()
+            gr.capture_end()
+        torch.cuda.synchronize()
+        graphs.append((gr, ctypes.c_void_p(gr.raw_cuda_graph_exec())))
+    res["graph_us"] = per_call_us(lambda: graph_flush(graphs[0][1]))
+    res["graph_kernel_node_us"] = per_call_us(lambda: graph_flush(graphs[1][1]))
+
+    g = DirectCollectives(slots)
+    res["direct_us"] = per_call_us(lambda: g.launch(0, 0, batch))
+    comm = g._comm
+
+    def in_stream(send, recv):
+        s = ctypes.c_void_p(_lib.stream_ptr(dev))
+        err = g.rccl.ncclAllReduce(ctypes.c_void_p(send), ctypes.c_void_p(recv), batch * 3, NCCL_FLOAT64, NCCL_SUM,
+                                   comm, s)
+        assert err == 0, err
+
+    res["direct_in_stream_us"] = per_call_us(lambda: in_stream(blk.data_ptr(), blk.data_ptr()))
+    res["direct_in_stream_out_of_place_us"] = per_call_us(lambda: in_stream(other.data_ptr(), blk.data_ptr()))
     torch.cuda.synchronize()
     blk.fill_(1.0)
     other.fill_(2.0)
-    direct(other.data_ptr(), blk.data_ptr())
+    in_stream(other.data_ptr(), blk.data_ptr())
     torch.cuda.synchronize()
-    res["direct_out_of_place_result_ok"] = bool(torch.equal(blk, other))
+    res["out_of_place_result_ok"] = bool(torch.equal(blk, other))
 
     s = ctypes.c_void_p(_lib.stream_ptr(dev))
     res["hipEventRecord_us"] = per_call_us(lambda: hip.hipEventRecord(ev_in, s))
     res["hipStreamWaitEvent_us"] = per_call_us(lambda: hip.hipStreamWaitEvent(cs, ev_in, 0))
-    ex = g.graphs[(0, 0, batch)][1]
-    res["hipGraphLaunch_kernel_node_us"] = per_call_us(lambda: hip.hipGraphLaunch(ex, cs))
+    res["hipGraphLaunch_kernel_node_us"] = per_call_us(lambda: hip.hipGraphLaunch(graphs[1][1], cs))
     res["stream_ptr_us"] = per_call_us(lambda: _lib.stream_ptr(dev))
     print(json.dumps(res), flush=True)
     torch.cuda.synchronize()
-    del g, proxy
+    del g, graphs
 dist.destroy_process_group()

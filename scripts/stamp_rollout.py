@@ -31,14 +31,15 @@ buf = torch.zeros(3, dtype=torch.float64, device=dev)
 for _ in range(20):
     p(buf.data_ptr())
 torch.cuda.synchronize()
-waves = min((n + 63) // 64, 1024)
 rows = []
 for rep in range(30):
     p(buf.data_ptr())
     torch.cuda.synchronize()
     h = np.zeros(1024 * SLOTS, dtype=np.uint64)
     assert lib.ouz_probe_stamps(h.ctypes.data, h.size) > 0
-    rows.append(h.reshape(1024, SLOTS)[:waves].astype(np.int64))
+    h = h.reshape(1024, SLOTS).astype(np.int64)
+    # the waves that stamp (the state waves of the split-wave form are every other wave): rows with a step start
+    rows.append(h[h[:, 13] > 0])
 st = np.concatenate(rows, 0)
 steps = np.diff(st[:, 13:30], axis=1)
 print(f"{task} N={n} fused rollout: {len(st)} wave samples; shader cycles per step (median over waves)")
@@ -57,6 +58,9 @@ else:
 if (st[:, 10:13] > 0).all() and (st[:, 2:5] > 0).all():
     print(f"  last step estimator: inputs->EKF {np.median(st[:, 10] - st[:, 2]):.0f}, EKF {np.median(st[:, 11] - st[:, 10]):.0f}, "
           f"PV {np.median(st[:, 12] - st[:, 11]):.0f}, guidance+Lee {np.median(st[:, 3] - st[:, 12]):.0f}")
+    pv = st[:, 12] - st[:, 11]
+    print("  last step PV phase over waves, percentiles 10/25/50/75/90:",
+          " ".join(f"{np.percentile(pv, q):.0f}" for q in (10, 25, 50, 75, 90)))
 print(f"  prologue: state loads issued -> landed {np.median(st[:, 1] - st[:, 0]):.0f}, landed -> first step "
       f"{np.median(st[:, 13] - st[:, 1]):.0f}; kernel entry (realtime) -> last wave exit "
       f"{np.median([int(r[:, 9].max() - r[:, 8].min()) * 10 for r in rows]):.0f} ns")

@@ -35,19 +35,20 @@ def _free_port():
     return port
 
 
-def test_graph_collectives_capture_on_rccl():
-    """The graph form of ReturnAllReduce's collectives (GraphCollectives, the default on RCCL at N > 1): capture
-    on a one-rank RCCL group, the construction-time check, and a replay of every captured row range."""
+def test_direct_collectives_on_rccl():
+    """The direct-RCCL form of ReturnAllReduce's collectives (DirectCollectives, the default on RCCL at N > 1) on
+    a one-rank RCCL group: set-up on the process group's communicator, the construction-time check, and every
+    row range of both blocks flushed and waited for."""
     if not torch.cuda.is_available():
         pytest.skip("needs a HIP device")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
-    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_graph_collective_worker.py")], env=env,
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "gpu_collective_worker.py")], env=env,
                        capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, (p.stdout + p.stderr)[-3000:]
     import json
     res = json.loads(p.stdout.strip().splitlines()[-1])
-    assert res == {"graphs": 2 * 4 * 5 // 2, "unchanged": True}
+    assert res == {"ranges": 2 * 4 * 5 // 2, "unchanged": True}
 
 
 @pytest.mark.parametrize("task,n,rollouts", [("QuadMixed", 4096, 12), ("QuadFault", 1000, 10)])

@@ -733,3 +733,52 @@ def test_c_host_example_runs():
     d = json.loads(out.stdout.strip().splitlines()[-1])
     assert d["step"] == 350 and d["obs0_finite"] == 1 and d["episodes"] >= 0
     assert d["env_steps_per_s"] > 5e7                                # BASELINE target on one GPU
+
+
+@pytest.mark.parametrize("task,n,off", [("QuadTracking", 4096, 0), ("EKFLeeLanded", 1000, 0), ("QuadMixed", 4096, 1300),
+                                        ("QuadTracking", 3000, 0)])
+def test_split_wave_rollout_matches_one_lane(ouz, task, n, off, monkeypatch):
+    """The split-wave estimator rollout (OUZ_SPLIT_PV=1, quad_pv_split.h: a state wave and a covariance wave per
+    64-slot tile, meeting in LDS) against the one-lane rollout kernel: storage rows, env buffers, the whole state
+    and the fused statistics bit for bit, over 16-, 32- (the longest launch), 7- and 16-step rollouts; and no
+    wait of the two waves ever gave up (ouz_split_timeouts).  Ragged tiles (1000 envs), a misaligned mixed shard
+    (tracking chunks split, the others one-lane in the state wave) and early resets (3000 envs, 30-step
+    episodes, 10-step convergence window)."""
+    import ctypes
+    from ouzelum_amd import _lib as L
+    kw = dict(seed=23, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True,
+              env_id_offset=off, num_envs_total=off + n)
+    if n == 3000:
+        kw.update(convergence_time=10, max_episode_length=30)
+    cnt = ctypes.c_uint32(0)
+    L.check(L.lib.ouz_split_timeouts(ctypes.byref(cnt), 1))
+    monkeypatch.setenv("OUZ_SPLIT_PV", "1")
+    a = ouz.make(**kw)
+    monkeypatch.setenv("OUZ_SPLIT_PV", "0")
+    b = ouz.make(**kw)
+    monkeypatch.delenv("OUZ_SPLIT_PV")
+    g = torch.Generator(device="cuda").manual_seed(5)
+    ring = (torch.rand((32, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
+    total = 0.0
+    for k_steps, drain in ((16, True), (32, False), (7, True), (16, True)):
+        outs = []
+        for env in (a, b):
+            st = (torch.full((k_steps, n, 13), -7.0, device="cuda"), torch.full((k_steps, n), -7.0, device="cuda"),
+                  torch.full((k_steps, n), -7, dtype=torch.int64, device="cuda"),
+                  torch.ones((k_steps, n), dtype=torch.bool, device="cuda"))
+            got = torch.full((3,), -1.0, dtype=torch.float64, device="cuda")
+            env.rollout(ring, k_steps, fused=True, storage=st, stats_out=got, drain=drain)
+            outs.append((st, got))
+        torch.cuda.synchronize()
+        for name, x, y in zip(("obs", "rew", "reset", "time_outs"), outs[0][0], outs[1][0]):
+            assert torch.equal(x, y), (k_steps, name)
+        assert torch.equal(outs[0][1], outs[1][1]), k_steps
+        assert torch.equal(a.frows(0, L.F_COUNT), b.frows(0, L.F_COUNT)), k_steps
+        assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT)), k_steps
+        for buf in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+            assert torch.equal(getattr(a, buf), getattr(b, buf)), buf
+        total += float(outs[0][1][1])
+    L.check(L.lib.ouz_split_timeouts(ctypes.byref(cnt), 1))
+    assert cnt.value == 0, f"{cnt.value} split-wave waits gave up"
+    if n == 3000:
+        assert total > 0, "no episode finished: the reset paths were not exercised"
