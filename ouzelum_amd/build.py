@@ -10,7 +10,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, "csrc", "quad_kernels.hip"), os.path.join(HERE, "csrc", "learner_kernels.hip")]
-DEPS = [*SRCS, os.path.join(HERE, "csrc", "quad_math.h"), os.path.join(HERE, "csrc", "philox.h"),
+DEPS = [*SRCS, *(os.path.join(HERE, "csrc", h) for h in ("quad_math.h", "philox.h", "quad_pv_ql.h", "quad_pv_split.h")),
         os.path.join(ROOT, "include", "ouzelum.h")]
 OUT = os.environ.get("OUZ_BUILD_OUT") or os.path.join(HERE, "libouzelum_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

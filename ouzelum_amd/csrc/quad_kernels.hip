@@ -734,6 +734,8 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     OUZ_STAMP(10, false);
     ekf_update(S.eq, S.eP, v3(gyr[0], gyr[1], gyr[2]), EkfQ{ang[0], ang[1], ang[2], ang[3]}, c.dt);
     OUZ_STAMP(11, false);
+    // SPW: the covariance wave starts this step's predict as soon as the attitude is known
+    if constexpr (SPW) pv_split_publish(*spl, conv ? qt : S.eq);
     EkfQ orient = S.eq;
     float pm[3] = {S.p.x, S.p.y, S.p.z}, vm[3] = {S.v.x, S.v.y, S.v.z}, am[3] = {lin_acc.x, lin_acc.y, lin_acc.z};
     if (conv) {
@@ -745,20 +747,34 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
-    if constexpr (QLN || SPW) {
-      // The covariance is in LDS and split over the env's lanes (QLN) or in the other wave (SPW): no register
-      // peak to park around.  The values the one-lane form parks go through an empty asm instead, which seals
-      // them the way the LDS round trip does (the code on either side of the PV step is then contracted the
-      // same way in every form, which keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
+    PvReal xd[9];   // SPW: the state estimate in f64 between its predict and the gains of this step's fixes
+    if constexpr (SPW) {
+      // The state wave: the same seal as the quad-lane form below, then the state predict; the fixes wait for
+      // the covariance wave's gains after the guidance, the rotation and the husky's step (none of which reads
+      // the estimate), right before the controller that does.
       float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
                         S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
                         S.dr_m, S.dr_i, S.dr_t};
-      if constexpr (SPW)
-        pv_state_split(*spl, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
-                       g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
-      else
-        pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
-                   g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
+      pv_split_predict(S.px, v3(am[0], am[1], am[2]), orient, c.dt, xd);
+      OUZ_STAMP(12, false);
+#pragma unroll
+      for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
+      S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);
+      S.q = Q4{vals[9], vals[10], vals[11], vals[12]};
+      target = v3(vals[13], vals[14], vals[15]);
+      S.wp = v3(vals[16], vals[17], vals[18]);
+      S.plat = make_float2(vals[19], vals[20]);
+      S.dr_m = vals[21]; S.dr_i = vals[22]; S.dr_t = vals[23];
+    } else if constexpr (QLN) {
+      // The covariance is in LDS and split over the env's lanes: no register peak to park around.  The values
+      // the one-lane form parks go through an empty asm instead, which seals them the way the LDS round trip
+      // does (the code on either side of the PV step is then contracted the same way in every form, which
+      // keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
+      float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
+                        S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
+                        S.dr_m, S.dr_i, S.dr_t};
+      pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
+                 g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
       OUZ_STAMP(12, false);
 #pragma unroll
       for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
@@ -814,6 +830,10 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     float T;
     V3 tau;
     R0 = quat_to_mat(S.q);   // after the PV step's register peak
+    if constexpr (SPW) {
+      if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);   // (not in the physics block below)
+      pv_split_correct(*spl, xd, S.px, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
+    }
     if (conv) lee_position_R(R0, S.p, S.v, S.w, wp, 0.0f, default_gains(), T, tau);
     else lee_position_R(R0, v3(S.px[0], S.px[1], S.px[2]), v3(S.px[3], S.px[4], S.px[5]), S.w, wp, 0.0f, default_gains(), T, tau);
     float fz = 2.0f * kGravity * T;
@@ -840,7 +860,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
-    if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);
+    if constexpr (TGT == TGT_TRAJ && !SPW) platform_step<CTRL, TGT>(a, sc, gid, S);
     if constexpr (CTRL == CTRL_RL) R0 = quat_to_mat(S.q);
     const DeckContact deck{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y};
     const float h = c.dt / (float)c.substeps;

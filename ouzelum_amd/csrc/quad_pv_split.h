@@ -11,8 +11,8 @@
 //     ring slot per step of the launch, and the count of steps published;
 //   * covariance -> state: the gains of a fix (S^-1 and the two other blocks' K rows, float64), one slot per
 //     fix type, and the step whose gains it holds.
-// The state wave waits only on a fix step, for the gains; the predict of every other step runs beside its
-// chain.  Every element is computed by the quad_math.h formulas (pv_state_predict, pv_cov_predict_t, pv_gain_t,
+// The state wave waits only on a fix step, for the gains, and only after the part of its step that does not
+// read the estimate (guidance, the rotation, the husky); the predict of every other step runs beside its chain.  Every element is computed by the quad_math.h formulas (pv_state_predict, pv_cov_predict_t, pv_gain_t,
 // pv_x_correct_t, pv_cov_correct_t) on the same operands as the one-lane pv_step, so the state and covariance
 // are bit for bit those of the one-lane kernels.
 //
@@ -58,20 +58,28 @@ __device__ __forceinline__ void split_wait(int* f, int v) {
   }
 }
 
-// The state wave's PV step: publish the attitude, predict the state, apply the gains of this step's fixes.
-// Same signature and results as pv_step for the state (the covariance is the other wave's).
-__device__ __forceinline__ void pv_state_split(const SplitLane& sl, float xf[9], V3 acc, EkfQ q, float dt,
-                                               bool pos_fix, V3 zp, bool vel_fix, V3 zv) {
+// The state wave's PV step, in three parts placed in its step (env_core): publish the attitude right after the
+// EKF; predict the state (f64, kept in xd); after the work that does not read the estimate, wait for and apply
+// the gains of this step's fixes and round to the f32 state.  The same operations on the same operands as
+// pv_step's state part.
+__device__ __forceinline__ void pv_split_publish(const SplitLane& sl, EkfQ q) {
   SplitPvLds& L = *sl.L;
   L.att[sl.k][sl.lane] = make_float4(q.w, q.x, q.y, q.z);
   split_publish(&L.att_count, sl.k + 1);
-  PvReal x[9];
+}
+
+__device__ __forceinline__ void pv_split_predict(const float xf[9], V3 acc, EkfQ q, float dt, PvReal x[9]) {
 #pragma unroll
   for (int k = 0; k < 9; ++k) x[k] = (PvReal)xf[k];
   const PvReal a[3] = {(PvReal)acc.x, (PvReal)acc.y, (PvReal)acc.z};
   const M3T<PvReal> M = pv_rot<PvReal>(q);
   const PvReal dtd = (PvReal)dt;
   pv_state_predict(x, a, M, dtd, dtd * dtd * PvReal(0.5));
+}
+
+__device__ __forceinline__ void pv_split_correct(const SplitLane& sl, PvReal x[9], float xf[9], bool pos_fix, V3 zp,
+                                                 bool vel_fix, V3 zv) {
+  SplitPvLds& L = *sl.L;
   M3T<PvReal> Si;
   PvReal KA[3][3], KB[3][3];
   const auto read_gains = [&](int f) {
