@@ -450,9 +450,6 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   // i: env index (the class layout's env-order buffers are not lane-contiguous)
   const int64_t rv = CLS ? a.rst_in[i] : (a.rst_in + S.T.first)[S.T.l];
   const uint32_t tv = CLS ? a.to_in[i] : (a.to_in + S.T.first)[S.T.l];
-  S.rst = rv != 0;
-  // flags read from another buffer than the outputs (streamed rollout): the outputs are always written
-  S.flags_clear = (rv == 0) & (tv == 0u) & (a.rst_in == a.reset);
   // NTL: non-temporal state loads (large N: see nt_loads_default)
   const auto L = [&](int f) -> float { return NTL ? ld_nt(S.T, f) : ld(S.T, f); };
   const auto LI = [&](int f) -> int32_t { return NTL ? ldi_nt(S.T, f) : ldi(S.T, f); };
@@ -507,6 +504,11 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
     S.plat = make_float2(0.0f, 0.0f);
   }
   S.plat_v = make_float2(0.0f, 0.0f);
+  // The flags are used last: a use right after their loads made the compiler wait for every load issued so
+  // far and issue the conditional loads above (DR scales, landing flag) in a second memory round trip.
+  S.rst = rv != 0;
+  // flags read from another buffer than the outputs (streamed rollout): the outputs are always written
+  S.flags_clear = (rv == 0) & (tv == 0u) & (a.rst_in == a.reset);
 }
 
 template <int CTRL, int TGT, bool QLN = false>
@@ -1065,18 +1067,19 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP_RT(8);
   OUZ_STAMP(0, false);
   S.T = tile_of(a, i);   // outside any divergent branch, so the base pointers stay scalar
-  if (valid) env_load<CTRL, TGT, CLS, NTL, QLN || SPW>(a, e, tp, S, ctx[0].actions);
-  if constexpr (QLN) {
-    if (valid) pv_lds_load(ql, [&](int f) { return ld(S.T, OUZ_F_PV_P + f); });
-    ql_sync();
-  }
-  // fused statistics: the episode accumulators of earlier (unfused) steps, in flight with the state
+  // fused statistics: the episode accumulators of earlier (unfused) steps, issued first so that they are in
+  // flight with the state (issued after it, they were a second memory round trip of the prologue)
   float ep_sum_old = 0.0f;
   int32_t ep_cnt_old = 0, ep_len_old = 0;
   if (MULTI && stats_mode && vout) {
     ep_sum_old = ld(S.T, OUZ_F_EP_SUM);
     ep_cnt_old = ldi(S.T, OUZ_I_EP_CNT);
     ep_len_old = ldi(S.T, OUZ_I_EP_LEN);
+  }
+  if (valid) env_load<CTRL, TGT, CLS, NTL, QLN || SPW>(a, e, tp, S, ctx[0].actions);
+  if constexpr (QLN) {
+    if (valid) pv_lds_load(ql, [&](int f) { return ld(S.T, OUZ_F_PV_P + f); });
+    ql_sync();
   }
   OUZ_STAMP(1, true);
   if constexpr (PRE) {
