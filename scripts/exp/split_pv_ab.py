@@ -1,5 +1,5 @@
 """A/B of the split-wave estimator rollout (OUZ_SPLIT_PV=1, quad_pv_split.h) against the one-lane rollout kernel
-at the BASELINE sizes: fused 16-step rollout, GPU us per step back to back (bench.Runner), three interleaved
+at the BASELINE sizes: fused 16-step rollout and per-step kernel, GPU us per step back to back (bench.Runner), three interleaved
 rounds, a bitwise check of the states after the same rollouts, and the split's give-up counter.
 
     python scripts/exp/split_pv_ab.py [tasks...]
@@ -28,9 +28,11 @@ for rnd in range(3):
             run = B.Runner(task, 4096, dev, 1234, 0, 1, ReturnAllReduce(dev, batch=1))
             run.rollouts(64)
             fused = run.back_to_back_us(fused=True, launches=40)
+            step = run.back_to_back_us(fused=False, launches=40)
             torch.cuda.synchronize()
             states[split] = run.env.fstate.clone()
-            print(json.dumps({"round": rnd, "task": task, "split_pv": split, "fused_us_per_step": round(fused, 3)}),
+            print(json.dumps({"round": rnd, "task": task, "split_pv": split, "fused_us_per_step": round(fused, 3),
+                              "step_kernel_us": round(step, 3)}),
                   flush=True)
             del run
         print(json.dumps({"task": task, "bitwise_equal_states": bool(torch.equal(states[0], states[1]))}), flush=True)
