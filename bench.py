@@ -478,6 +478,8 @@ def config_entry(letter, task, n, res, run, sweep=None):
     us_b2b_step = run.back_to_back_us(fused=False)
     e = {"config": letter, "task": task, "num_envs_per_gpu": n, "value": round(res["value"], 1),
          "unit": "env-steps/s", "ms_per_step": round(res["ms_per_step"], 5),
+         # the PV filter's covariance step runs in f64, the rest of the step in f32
+         "dtype": "f32 + f64 PV" if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else "f32",
          "roofline": {**roofline_entry("rollout", task, n, res["kernel_us"], RING),
                       "kernel_us_source": "HIP events on the step stream around the timed region / steps",
                       "kernel_us_back_to_back": round(us_b2b, 3)}}
