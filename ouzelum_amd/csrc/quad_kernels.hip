@@ -193,6 +193,7 @@ struct StepArgs {
   int32_t nt_loads;            // step kernels: non-temporal state loads (large N: nt_loads_default)
   int32_t quad;                // trigger-class layout: the quad-lane estimator kernels (OUZ_QUAD_LANE=1; quad_pv_ql.h)
   int32_t split;               // trigger-class layout: the split-wave estimator rollout (OUZ_SPLIT_PV; quad_pv_split.h)
+  int32_t outw;                // latency-regime rollouts with an output wave (OUZ_OUT_WAVE; out_wave)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
@@ -511,14 +512,15 @@ __device__ __forceinline__ void env_load(const StepArgs& a, int i, const TaskPar
   S.flags_clear = (rv == 0) & (tv == 0u) & (a.rst_in == a.reset);
 }
 
-template <int CTRL, int TGT, bool QLN = false>
+// EPW: this wave owns the episode-tracking fields (false for the state wave of a rollout with an output wave)
+template <int CTRL, int TGT, bool QLN = false, bool EPW = true>
 __device__ __forceinline__ void env_store(const StepArgs& a, int i, const TaskParams& tp, const EnvRegs<CTRL, TGT>& S) {
   st3(S.T, OUZ_F_P, S.p);
   st(S.T, OUZ_F_Q, S.q.x); st(S.T, OUZ_F_Q + 1, S.q.y); st(S.T, OUZ_F_Q + 2, S.q.z); st(S.T, OUZ_F_Q + 3, S.q.w);
   st3(S.T, OUZ_F_V, S.v);
   st3(S.T, OUZ_F_W, S.w);
   sti(S.T, OUZ_I_PROGRESS, S.progress);
-  if (a.track_episodes) {
+  if (EPW && a.track_episodes) {
     st(S.T, OUZ_F_EP_RET, S.ep_ret);
     // accumulators: one lane owns each address, so a no-return atomic add is the same f32 / i32
     // read-add-write without a load round trip before the wave can retire
@@ -607,6 +609,22 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
   S.heading = th;
 }
 
+// compute_observations + compute_ingenuity_reward of the post-step state (ekf_lee_landed.py:653-723,
+// vec_task.py:351-353): one body for the one-wave step and the output wave (out_wave).
+__device__ __forceinline__ void obs_reward(const StepArgs& a, const StepCtx& sc, const TaskParams& tp, int task,
+                                           uint32_t gid, V3 p, Q4 q, V3 v, V3 w, V3 target, float* ob, float& rew,
+                                           float& dist) {
+  ob[0] = (target.x - p.x) / 3.0f; ob[1] = (target.y - p.y) / 3.0f; ob[2] = (target.z - p.z) / 3.0f;
+  ob[3] = q.x; ob[4] = q.y; ob[5] = q.z; ob[6] = q.w;
+  ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
+  ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
+  pomdp_apply<13>(ob, tp, task, a, sc, gid, SITE_OBS, false);
+  if (a.drn_mask & 1) dr_noise_apply<13>(ob, a.drn[0], a.seed, gid, sc.step, RNG_DRN_OBS);   // vec_task.py:351-352
+#pragma unroll
+  for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
+  rew = reward(p, target, q, w, dist);
+}
+
 // ---------------------------------------------------------------------------
 // One VecTask.step of one env on register state (mirrors oracle/quad_oracle.py::OracleEnv.step)
 // ---------------------------------------------------------------------------
@@ -614,11 +632,14 @@ __device__ __forceinline__ void platform_step(const StepArgs& a, const StepCtx& 
 // [6] (force, torque; body frame at the COM) that gym.simulate would integrate to `wrench`.
 // QLN: the quad-lane estimator (four lanes per env, the PV covariance in LDS at `ql`).
 // SPW: the state wave of the split-wave estimator (quad_pv_split.h): the covariance is the other wave's.
-template <int CTRL, int TGT, bool PRE = false, bool QLN = false, bool SPW = false>
+// OWV: a rollout with an output wave: the step stops at the done decision; the output wave forms the
+// observation, reward and episode statistics from the post-step state (out_wave), so `ob` / `rew` are not
+// written here and the step's target goes to *post_target.
+template <int CTRL, int TGT, bool PRE = false, bool QLN = false, bool SPW = false, bool OWV = false>
 __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid, int task,
                                          EnvRegs<CTRL, TGT>& S, float* ob, float& rew, bool& rs, bool& timeout,
                                          float* wrench = nullptr, const PvQl* ql = nullptr,
-                                         const SplitLane* spl = nullptr) {
+                                         const SplitLane* spl = nullptr, V3* post_target = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const EnvConsts& c = a.c;
   const bool rst = S.rst;
@@ -882,25 +903,37 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     target.y = S.plat.y;
     target.z = 0.377f;
   }
-  const V3 p = S.p, v = S.v, w = S.w;
-  const Q4 q = S.q;
-  ob[0] = (target.x - p.x) / 3.0f; ob[1] = (target.y - p.y) / 3.0f; ob[2] = (target.z - p.z) / 3.0f;
-  ob[3] = q.x; ob[4] = q.y; ob[5] = q.z; ob[6] = q.w;
-  ob[7] = v.x * 0.5f; ob[8] = v.y * 0.5f; ob[9] = v.z * 0.5f;
-  ob[10] = w.x / kPiF; ob[11] = w.y / kPiF; ob[12] = w.z / kPiF;
-  pomdp_apply<13>(ob, tp, task, a, sc, gid, SITE_OBS, false);
-  if (a.drn_mask & 1) dr_noise_apply<13>(ob, a.drn[0], a.seed, gid, sc.step, RNG_DRN_OBS);   // vec_task.py:351-352
+  V3 p = S.p, v = S.v, w = S.w;
+  Q4 q = S.q;
+  // The observation / reward / done inputs go through an empty asm: the output wave (out_wave) reads them from
+  // LDS, and the same seal here keeps the compiler from contracting their arithmetic into the integrator's, so
+  // both forms evaluate obs_reward on the same opaque values (bitwise the same outputs).
+  {
+    float sv[16] = {p.x, p.y, p.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z, target.x, target.y, target.z};
 #pragma unroll
-  for (int k = 0; k < 13; ++k) ob[k] = fminf(fmaxf(ob[k], -5.0f), 5.0f);   // vec_task.py:353
+    for (int k = 0; k < 16; ++k) __asm__ volatile("" : "+v"(sv[k]));
+    p = v3(sv[0], sv[1], sv[2]);
+    q = Q4{sv[3], sv[4], sv[5], sv[6]};
+    v = v3(sv[7], sv[8], sv[9]);
+    w = v3(sv[10], sv[11], sv[12]);
+    target = v3(sv[13], sv[14], sv[15]);
+  }
   float dist;
-  rew = reward(p, target, q, w, dist);
+  if constexpr (OWV) {
+    dist = target_dist(p, target);
+    *post_target = target;
+  } else {
+    obs_reward(a, sc, tp, task, gid, p, q, v, w, target, ob, rew, dist);
+  }
   const bool timeout_len = S.progress >= tp.max_ep - 1;
   const bool die = dist > 8.0f || p.z < tp.z_die;
   rs = timeout_len || die;
   timeout = timeout_len && rs;                                             // vec_task.py:345
-  if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
-    S.ep_ret += rew;
-    if (rs) { S.ep_sum_add += S.ep_ret; S.ep_cnt_add += 1; S.ep_len_add += S.progress; S.ep_ret = 0.0f; }
+  if constexpr (!OWV) {
+    if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), summed on device
+      S.ep_ret += rew;
+      if (rs) { S.ep_sum_add += S.ep_ret; S.ep_cnt_add += 1; S.ep_len_add += S.progress; S.ep_ret = 0.0f; }
+    }
   }
   S.rst = rs;
   if (a.trace_cap > 0 && i == a.trace_env) {   // trajectory CSV row (ekf_lee_landed.py:667-674)
@@ -1017,6 +1050,34 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
   wave_lds_sync();
 }
 
+// The output wave of a latency-regime rollout.  The step's observation, reward, episode
+// statistics and output stores feed nothing the next step computes but the done flags, so a second wave of the
+// tile forms them from the post-step state while the state wave runs the next step's chain.  The state wave
+// publishes, per step, the post-step state (p, q, v, w, the target) with the progress counter and the done
+// flags into a ring slot; the output wave reads it, runs obs_reward / the episode tracking / the stores, and
+// releases the slot.  Waits: the state wave for a free slot (kOutRing steps ahead at most), the output wave for
+// a published step; both run the same K steps (quad_pv_split.h's split_wait, the same give-up bound).
+constexpr int kOutRing = 4;
+struct OutRingLds {
+  float4 post[kOutRing][4][64];   // p.xyz q.x | q.yzw v.x | v.yz w.xy | w.z target.xyz
+  int32_t meta[kOutRing][64];     // progress << 3 | flags_clear(step 0) << 2 | time_out << 1 | reset
+  int post_count;                 // steps published by the state wave
+  int consumed;                   // steps read by the output wave
+};
+
+__device__ __forceinline__ void out_publish(OutRingLds& R, int k, V3 p, Q4 q, V3 v, V3 w, V3 target,
+                                            int32_t progress, bool rs, bool to, bool fc0) {
+  if (k >= kOutRing) split_wait(&R.consumed, k - kOutRing + 1);
+  const int slot = k % kOutRing;
+  const uint32_t lane = threadIdx.x & 63u;
+  R.post[slot][0][lane] = make_float4(p.x, p.y, p.z, q.x);
+  R.post[slot][1][lane] = make_float4(q.y, q.z, q.w, v.x);
+  R.post[slot][2][lane] = make_float4(v.y, v.z, w.x, w.y);
+  R.post[slot][3][lane] = make_float4(w.z, target.x, target.y, target.z);
+  R.meta[slot][lane] = (progress << 3) | (fc0 ? 4 : 0) | (to ? 2 : 0) | (rs ? 1 : 0);
+  split_publish(&R.post_count, k + 1);
+}
+
 // Per-step reset count for the trace (metrics/<pomdp>_<prob>_ep_count.txt, ekf_lee_landed.py:315-320):
 // one atomic per wave with resets; env 0 clears the slot 32 steps ahead (fused rollouts run waves
 // at most 31 steps apart, and the capacity is >= 64).
@@ -1042,12 +1103,15 @@ struct LaneStats {
 // (the lanes 0-2 write the covariance elements they own).
 // SPW: the state wave of the split-wave estimator rollout (quad_pv_split.h; MULTI only): the covariance is
 // stepped by the workgroup's other wave (cov_wave), the two meet in `spl_lds`.
+// OWV: the state wave of a rollout with an output wave (out_wave): the step's outputs, episode tracking and
+// statistics are the output wave's; this wave publishes the post-step state into `orl` instead.
 template <int CTRL, int TGT, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QLN = false,
-          bool SPW = false>
+          bool SPW = false, bool OWV = false>
 __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                         size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
                                         bool direct = false, int stats_mode = 0, LaneStats* ls = nullptr,
-                                        float* wrench = nullptr, SplitPvLds* spl_lds = nullptr) {
+                                        float* wrench = nullptr, SplitPvLds* spl_lds = nullptr,
+                                        OutRingLds* orl = nullptr) {
   const TaskParams& tp = a.tp[tp_slot(task)];
   const uint32_t gid = a.env_offset + (uint32_t)e;
   // the env's outputs / statistics / state writes: every lane, or lane 0 of the quad
@@ -1056,6 +1120,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   PvQl ql{};
   SplitLane spl{spl_lds, 0, threadIdx.x & 63u};
   static_assert(!SPW || (MULTI && !PRE && !QLN && CTRL == CTRL_LEE_EST), "the split form is the estimator rollout's");
+  static_assert(!OWV || (MULTI && !PRE && !QLN), "the output wave is the rollout's");
   if constexpr (QLN) {
     static_assert(CTRL == CTRL_LEE_EST, "the quad-lane form is the estimator's");
     __shared__ double s_pv[16 * kPvLdsEnv];   // one 64-lane block = one wave = 16 envs
@@ -1071,7 +1136,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   // flight with the state (issued after it, they were a second memory round trip of the prologue)
   float ep_sum_old = 0.0f;
   int32_t ep_cnt_old = 0, ep_len_old = 0;
-  if (MULTI && stats_mode && vout) {
+  if (MULTI && !OWV && stats_mode && vout) {
     ep_sum_old = ld(S.T, OUZ_F_EP_SUM);
     ep_cnt_old = ldi(S.T, OUZ_I_EP_CNT);
     ep_len_old = ldi(S.T, OUZ_I_EP_LEN);
@@ -1111,6 +1176,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     // waits only for its own loads.  Measured effect small: SQ_WAIT_ANY 477 -> 463 wave quad-cycles per
     // LeeLanded step at 4096 envs (profiles/r02/sq_*); the per-step time is VALU/SALU issue.
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+    const bool fc0 = S.flags_clear;   // OWV: step 0's flag state, for the output wave
     for (int k = 0; k < K; ++k) {
       if (kStampSlots > 13 && k <= 16) OUZ_STAMP(13 + k, false);
       float ob[OUZ_NUM_OBS];
@@ -1120,10 +1186,17 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       // in the loop the buffers hold the previous step's flags: clear iff it was not done
       const bool flags_clear = vout && (k == 0 ? S.flags_clear : !did_reset);
       spl.k = k;
-      if (valid) env_core<CTRL, TGT, false, QLN, SPW>(a, ctx[k], e, gid, task, S, ob, rew, rs, to, nullptr, &ql, &spl);
+      V3 post_target = v3(0.0f, 0.0f, 0.0f);
+      if (valid)
+        env_core<CTRL, TGT, false, QLN, SPW, OWV>(a, ctx[k], e, gid, task, S, ob, rew, rs, to, nullptr, &ql, &spl,
+                                                  &post_target);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT, CLS>(ctx[k + 1].actions, S, e);   // next step's row, before emit
       trace_count(a, ctx[k].step, did_reset, i, e);
+      if constexpr (OWV) {
+        out_publish(*orl, k, S.p, S.q, S.v, S.w, post_target, S.progress, rs, to, fc0);
+        continue;
+      }
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
         o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
@@ -1145,7 +1218,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
     }
     if (kStampSlots > 13 && K <= 16) OUZ_STAMP(13 + K, false);
-    if (stats_mode && vout) {
+    if (!OWV && stats_mode && vout) {
       // RecordEpisodeStatisticsTorch over the rollout (PPO/utils.py:20-35) without a separate launch: this
       // lane's totals (accumulated before + finished in these K steps, same f32 adds as the atomics of
       // env_store) go to the grid reduction; drained accumulators are zeroed, kept ones written back.
@@ -1168,7 +1241,7 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
       S.ep_cnt_add = 0;   // env_store: no accumulator atomics
     }
   }
-  if (vout) env_store<CTRL, TGT, QLN || SPW>(a, i, tp, S);
+  if (vout) env_store<CTRL, TGT, QLN || SPW, !OWV>(a, i, tp, S);
   if constexpr (QLN) {
     if (valid) pv_lds_store(ql, [&](int f, float v) { st(S.T, OUZ_F_PV_P + f, v); });
   }
@@ -1176,8 +1249,104 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
   OUZ_STAMP_RT(9);
 }
 
+// The output wave of a rollout (see OutRingLds): per step, the observation, reward, episode tracking and output
+// stores of run_env's one-wave loop, from the state wave's published post-step state; at the end the episode
+// fields and the fused statistics.  Same functions (obs_reward, emit / emit_env) on the same values: the
+// outputs are bitwise those of the one-wave rollout.
+template <bool CLS>
+__device__ __forceinline__ void out_wave(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
+                                         size_t out_stride, float* wave_lds, int i, int e, bool valid, int task,
+                                         int stats_mode, LaneStats* ls, OutRingLds& R) {
+  const TaskParams& tp = a.tp[tp_slot(task)];
+  const uint32_t gid = a.env_offset + (uint32_t)e, lane = threadIdx.x & 63u;
+  const Tile T = tile_of(a, i);
+  const bool vout = valid;
+  float ep_sum_old = 0.0f, ep_ret = 0.0f, ep_sum_add = 0.0f;
+  int32_t ep_cnt_old = 0, ep_len_old = 0, ep_cnt_add = 0, ep_len_add = 0;
+  if (stats_mode && vout) {
+    ep_sum_old = ld(T, OUZ_F_EP_SUM);
+    ep_cnt_old = ldi(T, OUZ_I_EP_CNT);
+    ep_len_old = ldi(T, OUZ_I_EP_LEN);
+  }
+  if (valid && a.track_episodes) ep_ret = ld(T, OUZ_F_EP_RET);
+  bool prev_rs = false;
+  for (int k = 0; k < K; ++k) {
+    split_wait(&R.post_count, k + 1);
+    const int slot = k % kOutRing;
+    const float4 f0 = R.post[slot][0][lane], f1 = R.post[slot][1][lane], f2 = R.post[slot][2][lane],
+                 f3 = R.post[slot][3][lane];
+    const int32_t meta = R.meta[slot][lane];
+    split_publish(&R.consumed, k + 1);   // the values are in registers: the slot is free
+    const V3 p = v3(f0.x, f0.y, f0.z), v = v3(f1.w, f2.x, f2.y), w = v3(f2.z, f2.w, f3.x),
+             target = v3(f3.y, f3.z, f3.w);
+    const Q4 q = Q4{f0.w, f1.x, f1.y, f1.z};
+    const int32_t progress = meta >> 3;
+    const bool rs = (meta & 1) != 0, to = (meta & 2) != 0;
+    // run_env's flag state: at step 0 the buffers' own, later "not reset by the previous step"
+    const bool flags_clear = vout && (k == 0 ? (meta & 4) != 0 : !prev_rs);
+    float ob[OUZ_NUM_OBS];
+    float rew = 0.0f;
+    if (valid) {
+      float dist;
+      obs_reward(a, ctx[k], tp, task, gid, p, q, v, w, target, ob, rew, dist);
+      if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), as env_core
+        ep_ret += rew;
+        if (rs) { ep_sum_add += ep_ret; ep_cnt_add += 1; ep_len_add += progress; ep_ret = 0.0f; }
+      }
+    }
+    prev_rs = rs;
+    OutPtrs o = outs[0];
+    if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
+      o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
+      o.rew += (size_t)k * out_stride;
+      o.reset += (size_t)k * out_stride;
+      o.timeouts += (size_t)k * out_stride;
+      if (CLS) {
+        emit_env(o, e, vout, ob, rew, rs, to, false);
+        if (k == K - 1) emit_env(outs[1], e, vout, ob, rew, rs, to, false);
+      } else {
+        emit(o, wave_lds, i, a.n, vout, ob, rew, rs, to, false);
+        if (k == K - 1) emit(outs[1], wave_lds, i, a.n, vout, ob, rew, rs, to, false);
+      }
+    } else if (CLS) {
+      emit_env(o, e, vout, ob, rew, rs, to, flags_clear);
+    } else {
+      emit(o, wave_lds, i, a.n, vout, ob, rew, rs, to, false, flags_clear);
+    }
+  }
+  if (stats_mode && vout) {   // run_env's fused statistics
+    const float s_tot = ep_sum_old + ep_sum_add;
+    const int32_t c_tot = ep_cnt_old + ep_cnt_add, l_tot = ep_len_old + ep_len_add;
+    ls->sum += (double)s_tot;
+    ls->cnt += (double)c_tot;
+    ls->len += (double)l_tot;
+    if (stats_mode == 2) {
+      if (ep_cnt_old) {
+        st(T, OUZ_F_EP_SUM, 0.0f);
+        sti(T, OUZ_I_EP_CNT, 0);
+        sti(T, OUZ_I_EP_LEN, 0);
+      }
+    } else if (ep_cnt_add) {
+      st(T, OUZ_F_EP_SUM, s_tot);
+      sti(T, OUZ_I_EP_CNT, c_tot);
+      sti(T, OUZ_I_EP_LEN, l_tot);
+    }
+    ep_cnt_add = 0;
+  }
+  if (vout && a.track_episodes) {   // env_store's episode fields
+    st(T, OUZ_F_EP_RET, ep_ret);
+    if (ep_cnt_add) {
+      atomicAdd(&T.f[(uint32_t)OUZ_F_EP_SUM * 64u + T.l], ep_sum_add);
+      atomicAdd(&T.iv[(uint32_t)OUZ_I_EP_CNT * 64u + T.l], ep_cnt_add);
+      atomicAdd(&T.iv[(uint32_t)OUZ_I_EP_LEN * 64u + T.l], ep_len_add);
+    }
+  }
+}
+
 constexpr int kMaxRolloutChunk = 32;
 constexpr bool kSplitDefault = true;    // the split-wave estimator rollout is the default
+constexpr bool kOutWaveDefault = true;  // the output wave in the latency-regime rollouts
+constexpr int kOutWaveMaxSlots = 16384;
 static_assert(kSplitRing >= kMaxRolloutChunk, "one attitude slot per step of a launch");
 
 // The covariance wave of the split-wave estimator rollout (quad_pv_split.h): the PV covariance of the tile's 64
@@ -1290,7 +1459,7 @@ __host__ __device__ constexpr bool quad_lane_kernel(int task, bool cls) {
 }
 
 template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QUAD = false,
-          bool SPW = false>
+          bool SPW = false, bool OWV = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
@@ -1298,45 +1467,82 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
   float* wave_lds = reinterpret_cast<float*>(s_obs4) + (threadIdx.x & ~63) * OUZ_NUM_OBS;
   const int sm = (MULTI && rst) ? rst->mode : 0;
   LaneStats ls{0.0, 0.0, 0.0};
-  if constexpr (SPW && quad_lane_kernel(TASK, CLS)) {
-    // The split-wave estimator rollout (quad_pv_split.h): 128-thread blocks, one per 64-slot tile; wave 0 steps
-    // the tile's envs, wave 1 their PV covariance.
-    static_assert(MULTI && !PRE && !QUAD, "the split form is the estimator rollout's");
-    __shared__ SplitPvLds s_split;
+  if constexpr (SPW || OWV) {
+    // Multi-wave rollouts, one workgroup per 64-slot tile: wave 0 steps the tile's envs; with SPW (the
+    // estimator's trigger-class layout, quad_pv_split.h) wave 1 steps their PV covariance; with OWV the last
+    // wave forms the outputs (out_wave).
+    static_assert(MULTI && !PRE && !QUAD, "the multi-wave forms are the rollout's");
+    static_assert(!SPW || quad_lane_kernel(TASK, CLS), "the split form is the estimator's class layout");
+    SplitPvLds* spl = nullptr;
+    OutRingLds* orl = nullptr;
+    if constexpr (SPW) {
+      __shared__ SplitPvLds s_split;
+      spl = &s_split;
+    }
+    if constexpr (OWV) {
+      __shared__ OutRingLds s_out;
+      orl = &s_out;
+    }
     if (threadIdx.x == 0) {
-      s_split.att_count = 0;
-      s_split.gain_step[0] = 0;
-      s_split.gain_step[1] = 0;
+      if (spl) {
+        spl->att_count = 0;
+        spl->gain_step[0] = 0;
+        spl->gain_step[1] = 0;
+      }
+      if (orl) {
+        orl->post_count = 0;
+        orl->consumed = 0;
+      }
     }
     __syncthreads();
-    const int tile = (int)blockIdx.x, i = tile * 64 + (int)(threadIdx.x & 63u);
-    int e;
+    const int tile = (int)blockIdx.x, i = tile * 64 + (int)(threadIdx.x & 63u), role = (int)(threadIdx.x >> 6);
+    int e = i;
     int chunk_task = TASK;
-    if constexpr (TASK == OUZ_TASK_MIXED) {
+    if constexpr (CLS && TASK == OUZ_TASK_MIXED) {
       const int64_t e64 = mixed_slot_env(a.env_offset, i);
       e = (e64 >= 0 && e64 < a.n) ? (int)e64 : a.n;
       chunk_task = mixed_chunk_task(a.env_offset / kClassBlock + (uint32_t)(tile * 64) / kClassBlock);
-    } else {
+    } else if constexpr (CLS) {
       e = slot_env(i);
     }
     const bool valid = e < a.n;
-    constexpr int TGT = TASK == OUZ_TASK_EKF_LEE_LANDED ? TGT_PLATFORM : TGT_TRAJ;
-    if (threadIdx.x < 64u) {
-      if (chunk_task != OUZ_TASK_LEE_LANDED && chunk_task != OUZ_TASK_FAULT)
-        run_env<CTRL_LEE_EST, TGT, true, false, true, false, false, true>(
-            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK == OUZ_TASK_MIXED ? OUZ_TASK_TRACKING : TASK,
-            false, sm, &ls, nullptr, &s_split);
-      else if constexpr (TASK == OUZ_TASK_MIXED) {
-        if (chunk_task == OUZ_TASK_LEE_LANDED)
-          run_env<CTRL_LEE_TRUE, TGT_PLATFORM, true, false, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
-                                                                 OUZ_TASK_LEE_LANDED, false, sm, &ls);
+    const int run_task = TASK == OUZ_TASK_MIXED ? chunk_task : TASK;
+    constexpr int kOutRole = SPW ? 2 : 1;
+    if (role == 0) {
+      if constexpr (TASK == OUZ_TASK_OUZELUM || TASK == OUZ_TASK_FAULT)
+        run_env<CTRL_RL, TGT_GOAL, true, false, CLS, false, false, false, OWV>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, nullptr, nullptr, orl);
+      else if constexpr (TASK == OUZ_TASK_LEE_LANDED)
+        run_env<CTRL_LEE_TRUE, TGT_PLATFORM, true, false, CLS, false, false, false, OWV>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, nullptr, nullptr, orl);
+      else if constexpr (TASK == OUZ_TASK_LANDING)
+        run_env<CTRL_RL, TGT_TRAJ, true, false, CLS, false, false, false, OWV>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, nullptr, nullptr, orl);
+      else if constexpr (TASK == OUZ_TASK_EKF_LEE_LANDED)
+        run_env<CTRL_LEE_EST, TGT_PLATFORM, true, false, CLS, false, false, SPW, OWV>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, nullptr, spl, orl);
+      else if constexpr (TASK == OUZ_TASK_TRACKING)
+        run_env<CTRL_LEE_EST, TGT_TRAJ, true, false, CLS, false, false, SPW, OWV>(
+            a, ctx, K, outs, out_stride, wave_lds, i, e, valid, TASK, false, sm, &ls, nullptr, spl, orl);
+      else if constexpr (TASK == OUZ_TASK_MIXED && CLS) {
+        if (chunk_task == OUZ_TASK_TRACKING)
+          run_env<CTRL_LEE_EST, TGT_TRAJ, true, false, true, false, false, SPW, OWV>(
+              a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_TRACKING, false, sm, &ls, nullptr, spl, orl);
+        else if (chunk_task == OUZ_TASK_LEE_LANDED)
+          run_env<CTRL_LEE_TRUE, TGT_PLATFORM, true, false, true, false, false, false, OWV>(
+              a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_LEE_LANDED, false, sm, &ls, nullptr, nullptr,
+              orl);
         else
-          run_env<CTRL_RL, TGT_GOAL, true, false, true>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid,
-                                                       OUZ_TASK_FAULT, false, sm, &ls);
+          run_env<CTRL_RL, TGT_GOAL, true, false, true, false, false, false, OWV>(
+              a, ctx, K, outs, out_stride, wave_lds, i, e, valid, OUZ_TASK_FAULT, false, sm, &ls, nullptr, nullptr, orl);
       }
-      if (sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // the state waves of the exact grid
-    } else if (chunk_task != OUZ_TASK_LEE_LANDED && chunk_task != OUZ_TASK_FAULT) {
-      cov_wave(a, ctx, K, i, e, valid, s_split);
+      if (!OWV && sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // the state waves of the exact grid
+    } else if (SPW && role == 1) {
+      if (run_task == OUZ_TASK_TRACKING || run_task == OUZ_TASK_EKF_LEE_LANDED)
+        cov_wave(a, ctx, K, i, e, valid, *spl);
+    } else if (OWV && role == kOutRole) {
+      out_wave<CLS>(a, ctx, K, outs, out_stride, wave_lds, i, e, valid, run_task, sm, &ls, *orl);
+      if (sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // the output waves of the exact grid
     }
     return;
   }
@@ -1452,10 +1658,10 @@ __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx
 
 // ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.  SPW: the split-wave
 // estimator form (quad_pv_split.h), 128-thread blocks.
-template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false>
+template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false, bool OWV = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true, false, CLS, false, QUAD, SPW>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+  step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
@@ -2076,6 +2282,11 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     // the split-wave estimator rollout (quad_pv_split.h): bit-identical results; OUZ_SPLIT_PV=0 / 1 overrides
     const char* sp = std::getenv("OUZ_SPLIT_PV");
     a.split = (a.cls && !a.quad && (sp ? std::atoi(sp) != 0 : kSplitDefault)) ? 1 : 0;
+    // the output wave while the rollout's waves stay within one per SIMD (256 tiles); OUZ_OUT_WAVE=0 / 1 overrides
+    const char* ow = std::getenv("OUZ_OUT_WAVE");
+    // (the mixed curriculum has the output-wave form in its class layout only)
+    const bool ow_size = a.n_slots <= kOutWaveMaxSlots && !a.quad && (a.cls || cfg->task != OUZ_TASK_MIXED);
+    a.outw = (ow_size && (ow ? std::atoi(ow) != 0 : kOutWaveDefault)) ? 1 : 0;
   }
   {
     const char* rs = std::getenv("OUZ_ROLLOUT_STREAM");
@@ -2189,8 +2400,10 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
       else hipLaunchKernelGGL((quad_rollout_kernel<T, true, true>), g4, b, 0, s, a, r);
       return;
     }
-    if (a.cls && a.split && !single) {   // the split-wave estimator rollout: two waves per 64-slot tile
-      hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, true>), g, dim3(128), 0, s, a, r);
+    if (a.cls && !single && (a.split || a.outw)) {   // multi-wave rollouts: one workgroup per 64-slot tile
+      if (a.split && a.outw) hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, true, true>), g, dim3(192), 0, s, a, r);
+      else if (a.split) hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, true, false>), g, dim3(128), 0, s, a, r);
+      else hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, false, true>), g, dim3(128), 0, s, a, r);
       return;
     }
     if (a.cls) {
@@ -2201,6 +2414,8 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   }
   if (single && a.nt_loads) hipLaunchKernelGGL((quad_step_kernel<T, false, true>), g, b, 0, s, a, r.ctx[0]);
   else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false>), g, b, 0, s, a, r.ctx[0]);
+  else if (T != OUZ_TASK_MIXED && a.outw)
+    hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, T != OUZ_TASK_MIXED>), g, dim3(128), 0, s, a, r);
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 

@@ -701,9 +701,14 @@ OUZ_HD void pv_correct(float xf[9], float Pf[45], V3 z, float r) {
 // Reward / observation
 // ---------------------------------------------------------------------------
 // compute_ingenuity_reward (tasks/ekf_lee_landed.py:692-723).
-OUZ_HD float reward(V3 p, V3 target, Q4 q, V3 w, float& dist) {
+// distance to the target: the reward's position term and the die test (one formula for both)
+OUZ_HD float target_dist(V3 p, V3 target) {
   V3 d = target - p;
-  dist = sqrtf(dot(d, d));
+  return sqrtf(dot(d, d));
+}
+
+OUZ_HD float reward(V3 p, V3 target, Q4 q, V3 w, float& dist) {
+  dist = target_dist(p, target);
   float pos_r = 1.0f / (1.0f + dist * dist);
   float ups_z = 2.0f * q.w * q.w - 1.0f + q.z * q.z * 2.0f;      // quat_axis(q, 2).z
   float tilt = fabsf(1.0f - ups_z);

@@ -782,3 +782,67 @@ def test_split_wave_rollout_matches_one_lane(ouz, task, n, off, monkeypatch):
     assert cnt.value == 0, f"{cnt.value} split-wave waits gave up"
     if n == 3000:
         assert total > 0, "no episode finished: the reset paths were not exercised"
+
+
+@pytest.mark.parametrize("task,n,off", [("LeeLanded", 4096, 0), ("QuadFault", 1000, 0), ("Ouzelum", 200, 0),
+                                        ("Landing", 4096, 0), ("QuadTracking", 3000, 0), ("EKFLeeLanded", 1000, 0),
+                                        ("QuadMixed", 4096, 1300)])
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_output_wave_rollout_matches_one_wave(ouz, task, n, off, split, monkeypatch):
+    """The latency-regime rollout with an output wave (OUZ_OUT_WAVE=1: the tile's last wave forms the
+    observations, rewards, episode statistics and output stores from the state wave's published post-step state)
+    against the one-wave rollout (OUZ_OUT_WAVE=0), with and without the estimator's split-wave covariance: storage
+    rows, env buffers, the whole state and the fused statistics bit for bit, over 16-, 32-, 7- and 16-step
+    rollouts with drained and kept statistics, then rollouts without storage (outputs into the env buffers, whose
+    flags a not-reset env may keep) and without statistics; and no wait gave up (ouz_split_timeouts)."""
+    import ctypes
+    from ouzelum_amd import _lib as L
+    if split == "1" and task not in ("QuadTracking", "EKFLeeLanded", "QuadMixed"):
+        pytest.skip("the split-wave covariance is the estimator's")
+    kw = dict(seed=29, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True,
+              env_id_offset=off, num_envs_total=off + n)
+    if task in ("QuadTracking", "QuadMixed", "EKFLeeLanded"):
+        kw["convergence_time"] = 10
+    kw["max_episode_length"] = 30   # episodes end inside the test: the reset and statistics paths run
+    cnt = ctypes.c_uint32(0)
+    L.check(L.lib.ouz_split_timeouts(ctypes.byref(cnt), 1))
+    monkeypatch.setenv("OUZ_SPLIT_PV", split)
+    monkeypatch.setenv("OUZ_OUT_WAVE", "1")
+    a = ouz.make(**kw)
+    monkeypatch.setenv("OUZ_OUT_WAVE", "0")
+    b = ouz.make(**kw)
+    monkeypatch.delenv("OUZ_OUT_WAVE")
+    monkeypatch.delenv("OUZ_SPLIT_PV")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    ring = (torch.rand((32, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
+
+    def same_state(tag):
+        torch.cuda.synchronize()
+        assert torch.equal(a.frows(0, L.F_COUNT), b.frows(0, L.F_COUNT)), tag
+        assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT)), tag
+        for buf in ("obs_buf", "rew_buf", "reset_buf", "timeout_buf"):
+            assert torch.equal(getattr(a, buf), getattr(b, buf)), (tag, buf)
+
+    total = 0.0
+    for k_steps, drain in ((16, True), (32, False), (7, True), (16, True)):
+        outs = []
+        for env in (a, b):
+            st = (torch.full((k_steps, n, 13), -7.0, device="cuda"), torch.full((k_steps, n), -7.0, device="cuda"),
+                  torch.full((k_steps, n), -7, dtype=torch.int64, device="cuda"),
+                  torch.ones((k_steps, n), dtype=torch.bool, device="cuda"))
+            got = torch.full((3,), -1.0, dtype=torch.float64, device="cuda")
+            env.rollout(ring, k_steps, fused=True, storage=st, stats_out=got, drain=drain)
+            outs.append((st, got))
+        torch.cuda.synchronize()
+        for name, x, y in zip(("obs", "rew", "reset", "time_outs"), outs[0][0], outs[1][0]):
+            assert torch.equal(x, y), (k_steps, name)
+        assert torch.equal(outs[0][1], outs[1][1]), k_steps
+        same_state(f"{k_steps}-step rollout")
+        total += float(outs[0][1][1])
+    for k_steps in (16, 5):   # no storage, no statistics: every step's outputs into the env buffers
+        a.rollout(ring, k_steps, fused=True)
+        b.rollout(ring, k_steps, fused=True)
+        same_state(f"{k_steps}-step rollout without storage")
+    L.check(L.lib.ouz_split_timeouts(ctypes.byref(cnt), 1))
+    assert cnt.value == 0, f"{cnt.value} multi-wave waits gave up"
+    assert total > 0, "no episode finished: the episode statistics were not exercised"
