@@ -19,9 +19,13 @@ FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wn
          # f32 divide / sqrt to ~1-2 ulp instead of correctly rounded: -14 % VALU in the step kernel,
          # well inside the parity tolerances.  f64 (PV filter) and the RNG (__f*_rn) are unaffected.
          "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-         # FMA contraction stays on everywhere except where a `#pragma clang fp contract(off)` asks for
-         # torch's one-rounding-per-op order (RNG uniforms, GAE): __fmul_rn/__fadd_rn are plain operators in HIP.
-         "-ffp-contract=fast-honor-pragmas",
+         # FMA contraction within an expression (a * b + c), never across statements, except where a
+         # `#pragma clang fp contract(off)` asks for torch's one-rounding-per-op order (RNG uniforms, GAE):
+         # __fmul_rn/__fadd_rn are plain operators in HIP.  With cross-statement fusion (fast) the rounding
+         # of the step depended on the code around it (basic-block boundaries, a value's other uses), so the
+         # kernel forms (one-lane / split-wave / quad-lane / output-wave, step / rollout) needed empty-asm seals
+         # to stay bitwise equal; with "on" they are equal by construction.
+         "-ffp-contract=on",
          # no SLP packing of f32 pairs into v_pk_*: on this per-lane scalar code it only adds register-pair
          # moves (v_mov -60 %, -5..7 % instructions per step phase) and ~40 VGPRs in the estimator kernels
          "-fno-slp-vectorize",

@@ -768,45 +768,22 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
       pomdp_apply<3>(pm, tp, task, a, sc, gid, SITE_POS, false);
       pomdp_apply<3>(vm, tp, task, a, sc, gid, SITE_VEL, false);
     }
+    if constexpr (SPW) OUZ_STAMP(5, false);
     // predict, position fix, velocity fix with R = 0 (PVFilter.py:76-79); shared trigger counters (:425-440)
     const uint64_t g = (uint64_t)sc.step * a.n_total + gid;
     PvReal xd[9];   // SPW: the state estimate in f64 between its predict and the gains of this step's fixes
     if constexpr (SPW) {
-      // The state wave: the same seal as the quad-lane form below, then the state predict; the fixes wait for
-      // the covariance wave's gains after the guidance, the rotation and the husky's step (none of which reads
-      // the estimate), right before the controller that does.
-      float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
-                        S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
-                        S.dr_m, S.dr_i, S.dr_t};
+      // The state wave: the state predict; the fixes wait for the covariance wave's gains after the guidance, the
+      // rotation and the husky's step (none of which reads the estimate), right before the controller that does.
+      // (Every form contracts only within an expression, -ffp-contract=on in build.py, so the split, quad-lane
+      // and one-lane forms round alike without the LDS round trip of the one-lane form's parking.)
       pv_split_predict(S.px, v3(am[0], am[1], am[2]), orient, c.dt, xd);
       OUZ_STAMP(12, false);
-#pragma unroll
-      for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
-      S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);
-      S.q = Q4{vals[9], vals[10], vals[11], vals[12]};
-      target = v3(vals[13], vals[14], vals[15]);
-      S.wp = v3(vals[16], vals[17], vals[18]);
-      S.plat = make_float2(vals[19], vals[20]);
-      S.dr_m = vals[21]; S.dr_i = vals[22]; S.dr_t = vals[23];
     } else if constexpr (QLN) {
-      // The covariance is in LDS and split over the env's lanes: no register peak to park around.  The values
-      // the one-lane form parks go through an empty asm instead, which seals them the way the LDS round trip
-      // does (the code on either side of the PV step is then contracted the same way in every form, which
-      // keeps them bit-identical: tests/test_gpu_env.py::test_large_n_matches_shards).
-      float vals[24] = {S.p.x, S.p.y, S.p.z, S.v.x, S.v.y, S.v.z, S.w.x, S.w.y, S.w.z, S.q.x, S.q.y, S.q.z,
-                        S.q.w, target.x, target.y, target.z, S.wp.x, S.wp.y, S.wp.z, S.plat.x, S.plat.y,
-                        S.dr_m, S.dr_i, S.dr_t};
+      // The covariance is in LDS and split over the env's lanes: no register peak to park around.
       pv_step_ql(*ql, S.px, v3(am[0], am[1], am[2]), orient, c.dt, g % 7u == 6u, v3(pm[0], pm[1], pm[2]),
                  g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
       OUZ_STAMP(12, false);
-#pragma unroll
-      for (int k = 0; k < 24; ++k) __asm__ volatile("" : "+v"(vals[k]));
-      S.p = v3(vals[0], vals[1], vals[2]); S.v = v3(vals[3], vals[4], vals[5]); S.w = v3(vals[6], vals[7], vals[8]);
-      S.q = Q4{vals[9], vals[10], vals[11], vals[12]};
-      target = v3(vals[13], vals[14], vals[15]);
-      S.wp = v3(vals[16], vals[17], vals[18]);
-      S.plat = make_float2(vals[19], vals[20]);
-      S.dr_m = vals[21]; S.dr_i = vals[22]; S.dr_t = vals[23];
     } else {
       // The float64 PV step is the register peak of the estimator kernels.  Everything the env holds
       // that the step does not read (true state, target, waypoint, platform, DR scales) is parked in
@@ -855,6 +832,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     R0 = quat_to_mat(S.q);   // after the PV step's register peak
     if constexpr (SPW) {
       if constexpr (TGT == TGT_TRAJ) platform_step<CTRL, TGT>(a, sc, gid, S);   // (not in the physics block below)
+      OUZ_STAMP(6, false);
       pv_split_correct(*spl, xd, S.px, g % 7u == 6u, v3(pm[0], pm[1], pm[2]), g % 3u == 0u, v3(vm[0], vm[1], vm[2]));
     }
     if (conv) lee_position_R(R0, S.p, S.v, S.w, wp, 0.0f, default_gains(), T, tau);
@@ -903,21 +881,10 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     target.y = S.plat.y;
     target.z = 0.377f;
   }
-  V3 p = S.p, v = S.v, w = S.w;
-  Q4 q = S.q;
-  // The observation / reward / done inputs go through an empty asm: the output wave (out_wave) reads them from
-  // LDS, and the same seal here keeps the compiler from contracting their arithmetic into the integrator's, so
-  // both forms evaluate obs_reward on the same opaque values (bitwise the same outputs).
-  {
-    float sv[16] = {p.x, p.y, p.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z, target.x, target.y, target.z};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) __asm__ volatile("" : "+v"(sv[k]));
-    p = v3(sv[0], sv[1], sv[2]);
-    q = Q4{sv[3], sv[4], sv[5], sv[6]};
-    v = v3(sv[7], sv[8], sv[9]);
-    w = v3(sv[10], sv[11], sv[12]);
-    target = v3(sv[13], sv[14], sv[15]);
-  }
+  // (the output wave, out_wave, forms the observation / reward from these values read back from LDS: with
+  // contraction only within expressions both forms round alike)
+  const V3 p = S.p, v = S.v, w = S.w;
+  const Q4 q = S.q;
   float dist;
   if constexpr (OWV) {
     dist = target_dist(p, target);
@@ -936,7 +903,7 @@ __device__ __forceinline__ void env_core(const StepArgs& a, const StepCtx& sc, i
     }
   }
   S.rst = rs;
-  if (a.trace_cap > 0 && i == a.trace_env) {   // trajectory CSV row (ekf_lee_landed.py:667-674)
+  if (!OWV && a.trace_cap > 0 && i == a.trace_env) {   // trajectory CSV row (ekf_lee_landed.py:667-674)
     float* t = a.trace + (size_t)(sc.step % (uint32_t)a.trace_cap) * 9;
     t[0] = p.x; t[1] = p.y; t[2] = p.z;
     t[3] = target.x; t[4] = target.y; t[5] = target.z;
@@ -1056,31 +1023,32 @@ __device__ __forceinline__ void emit(const OutPtrs& o, float* wave_lds, int i, i
 // publishes, per step, the post-step state (p, q, v, w, the target) with the progress counter and the done
 // flags into a ring slot; the output wave reads it, runs obs_reward / the episode tracking / the stores, and
 // releases the slot.  Waits: the state wave for a free slot (kOutRing steps ahead at most), the output wave for
-// a published step; both run the same K steps (quad_pv_split.h's split_wait, the same give-up bound).
-constexpr int kOutRing = 4;
+// a published step; both run the same K steps (quad_pv_split.h's split_wait, the same give-up bound).  The
+// slots are [field][lane] dwords, so the 16 values go out as 8 ds_write2st64_b32 straight from the registers
+// they are in (a float4 row per lane needed a register quad per store, i.e. 16 moves per step), and the state
+// wave re-reads the consumed count only when the count it last saw does not cover the slot it is about to reuse.
+constexpr int kOutRing = 8;
+constexpr int kOutFields = 16;   // p.xyz, q.xyzw, v.xyz, w.xyz, target.xyz
 struct OutRingLds {
-  float4 post[kOutRing][4][64];   // p.xyz q.x | q.yzw v.x | v.yz w.xy | w.z target.xyz
-  int32_t meta[kOutRing][64];     // progress << 3 | flags_clear(step 0) << 2 | time_out << 1 | reset
+  float post[kOutRing][kOutFields][64];
+  int32_t meta[kOutRing][64];     // progress << 4 | rst(step 0) << 3 | flags_clear(step 0) << 2 | time_out << 1 | reset
   int post_count;                 // steps published by the state wave
   int consumed;                   // steps read by the output wave
 };
 
-__device__ __forceinline__ void out_publish(OutRingLds& R, int k, V3 p, Q4 q, V3 v, V3 w, V3 target,
-                                            int32_t progress, bool rs, bool to, bool fc0) {
-  if (k >= kOutRing) split_wait(&R.consumed, k - kOutRing + 1);
+__device__ __forceinline__ void out_publish(OutRingLds& R, int k, int& seen, V3 p, Q4 q, V3 v, V3 w, V3 target,
+                                            int32_t progress, bool rs, bool to, bool fc0, bool rst0) {
+  if (k >= kOutRing && seen < k - kOutRing + 1) seen = split_wait(&R.consumed, k - kOutRing + 1);
   const int slot = k % kOutRing;
   const uint32_t lane = threadIdx.x & 63u;
-  R.post[slot][0][lane] = make_float4(p.x, p.y, p.z, q.x);
-  R.post[slot][1][lane] = make_float4(q.y, q.z, q.w, v.x);
-  R.post[slot][2][lane] = make_float4(v.y, v.z, w.x, w.y);
-  R.post[slot][3][lane] = make_float4(w.z, target.x, target.y, target.z);
-  R.meta[slot][lane] = (progress << 3) | (fc0 ? 4 : 0) | (to ? 2 : 0) | (rs ? 1 : 0);
+  const float f[kOutFields] = {p.x, p.y, p.z, q.x, q.y, q.z, q.w, v.x, v.y, v.z, w.x, w.y, w.z,
+                               target.x, target.y, target.z};
+#pragma unroll
+  for (int j = 0; j < kOutFields; ++j) R.post[slot][j][lane] = f[j];
+  R.meta[slot][lane] = (progress << 4) | (rst0 ? 8 : 0) | (fc0 ? 4 : 0) | (to ? 2 : 0) | (rs ? 1 : 0);
   split_publish(&R.post_count, k + 1);
 }
 
-// Per-step reset count for the trace (metrics/<pomdp>_<prob>_ep_count.txt, ekf_lee_landed.py:315-320):
-// one atomic per wave with resets; env 0 clears the slot 32 steps ahead (fused rollouts run waves
-// at most 31 steps apart, and the capacity is >= 64).
 __device__ __forceinline__ void trace_count(const StepArgs& a, uint32_t step, bool did_reset, int slot, int e) {
   if (a.trace_cap <= 0) return;
   const uint64_t m = __ballot(did_reset);
@@ -1176,7 +1144,8 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
     // waits only for its own loads.  Measured effect small: SQ_WAIT_ANY 477 -> 463 wave quad-cycles per
     // LeeLanded step at 4096 envs (profiles/r02/sq_*); the per-step time is VALU/SALU issue.
     __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-    const bool fc0 = S.flags_clear;   // OWV: step 0's flag state, for the output wave
+    const bool fc0 = S.flags_clear, rst0 = S.rst;   // OWV: step 0's flag / reset state, for the output wave
+    int out_seen = 0;                               // OWV: the output wave's consumed count last seen
     for (int k = 0; k < K; ++k) {
       if (kStampSlots > 13 && k <= 16) OUZ_STAMP(13 + k, false);
       float ob[OUZ_NUM_OBS];
@@ -1192,11 +1161,12 @@ __device__ __forceinline__ void run_env(const StepArgs& a, const StepCtx* ctx, i
                                                   &post_target);
       if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
       if (valid && k + 1 < K) load_actions<CTRL, TGT, CLS>(ctx[k + 1].actions, S, e);   // next step's row, before emit
-      trace_count(a, ctx[k].step, did_reset, i, e);
-      if constexpr (OWV) {
-        out_publish(*orl, k, S.p, S.q, S.v, S.w, post_target, S.progress, rs, to, fc0);
+      if constexpr (OWV) {   // (the reset counts of the trajectory log are the output wave's)
+        out_publish(*orl, k, out_seen, S.p, S.q, S.v, S.w, post_target, S.progress, rs, to, fc0, rst0);
+          if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
         continue;
       }
+      trace_count(a, ctx[k].step, did_reset, i, e);
       OutPtrs o = outs[0];
       if (out_stride) {   // rollout storage: step k of (K, N, ...) buffers; the env buffers get the last step
         o.obs += (size_t)k * out_stride * OUZ_NUM_OBS;
@@ -1271,22 +1241,34 @@ __device__ __forceinline__ void out_wave(const StepArgs& a, const StepCtx* ctx, 
   if (valid && a.track_episodes) ep_ret = ld(T, OUZ_F_EP_RET);
   bool prev_rs = false;
   for (int k = 0; k < K; ++k) {
+    if (kStampSlots > 13 && k <= 16) OUZ_STAMP(13 + k, false);
     split_wait(&R.post_count, k + 1);
+    if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
     const int slot = k % kOutRing;
-    const float4 f0 = R.post[slot][0][lane], f1 = R.post[slot][1][lane], f2 = R.post[slot][2][lane],
-                 f3 = R.post[slot][3][lane];
+    float f[kOutFields];
+#pragma unroll
+    for (int j = 0; j < kOutFields; ++j) f[j] = R.post[slot][j][lane];
     const int32_t meta = R.meta[slot][lane];
     split_publish(&R.consumed, k + 1);   // the values are in registers: the slot is free
-    const V3 p = v3(f0.x, f0.y, f0.z), v = v3(f1.w, f2.x, f2.y), w = v3(f2.z, f2.w, f3.x),
-             target = v3(f3.y, f3.z, f3.w);
-    const Q4 q = Q4{f0.w, f1.x, f1.y, f1.z};
-    const int32_t progress = meta >> 3;
+    const V3 p = v3(f[0], f[1], f[2]), v = v3(f[7], f[8], f[9]), w = v3(f[10], f[11], f[12]),
+             target = v3(f[13], f[14], f[15]);
+    const Q4 q = Q4{f[3], f[4], f[5], f[6]};
+    const int32_t progress = meta >> 4;
     const bool rs = (meta & 1) != 0, to = (meta & 2) != 0;
+    // run_env's trajectory-log reset count: the step's resets are the envs its previous step ended (step 0:
+    // the buffers' own flags)
+    trace_count(a, ctx[k].step, vout && (k == 0 ? (meta & 8) != 0 : prev_rs), i, e);
     // run_env's flag state: at step 0 the buffers' own, later "not reset by the previous step"
     const bool flags_clear = vout && (k == 0 ? (meta & 4) != 0 : !prev_rs);
     float ob[OUZ_NUM_OBS];
     float rew = 0.0f;
     if (valid) {
+      if (a.trace_cap > 0 && e == a.trace_env) {   // env_core's trajectory CSV row (ekf_lee_landed.py:667-674)
+        float* t = a.trace + (size_t)(ctx[k].step % (uint32_t)a.trace_cap) * 9;
+        t[0] = p.x; t[1] = p.y; t[2] = p.z;
+        t[3] = target.x; t[4] = target.y; t[5] = target.z;
+        t[6] = v.x; t[7] = v.y; t[8] = v.z;
+      }
       float dist;
       obs_reward(a, ctx[k], tp, task, gid, p, q, v, w, target, ob, rew, dist);
       if (a.track_episodes) {   // RecordEpisodeStatisticsTorch.step (PPO/utils.py:20-35), as env_core
@@ -1313,7 +1295,9 @@ __device__ __forceinline__ void out_wave(const StepArgs& a, const StepCtx* ctx, 
     } else {
       emit(o, wave_lds, i, a.n, vout, ob, rew, rs, to, false, flags_clear);
     }
+    if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
   }
+  if (kStampSlots > 13 && K <= 16) OUZ_STAMP(13 + K, false);
   if (stats_mode && vout) {   // run_env's fused statistics
     const float s_tot = ep_sum_old + ep_sum_add;
     const int32_t c_tot = ep_cnt_old + ep_cnt_add, l_tot = ep_len_old + ep_len_add;
@@ -1363,8 +1347,10 @@ __device__ __forceinline__ void cov_wave(const StepArgs& a, const StepCtx* ctx, 
     // the fix decisions of env_core's PV step (g % 7 == 6 position, g % 3 == 0 velocity), for the lanes the
     // state wave steps
     const uint64_t g = (uint64_t)ctx[k].step * a.n_total + gid;
+    if (kStampSlots > 13 && k <= 16) OUZ_STAMP(13 + k, false);
     pv_cov_split(L, k, lane, pf, a.c.dt, valid && g % 7u == 6u, valid && g % 3u == 0u);
   }
+  if (kStampSlots > 13 && K <= 16) OUZ_STAMP(13 + K, false);
   if (valid) {
 #pragma unroll
     for (int f = 0; f < 45; ++f) st(T, OUZ_F_PV_P + f, pf[f]);

@@ -48,11 +48,15 @@ struct SplitLane {
 __device__ __forceinline__ void split_publish(int* f, int v) {
   __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void split_wait(int* f, int v) {
-  for (uint32_t it = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v; ++it) {
+// Waits until *f >= v; returns the count it saw (v after a give-up), so that a caller may skip later waits the
+// count already covers.
+__device__ __forceinline__ int split_wait(int* f, int v) {
+  for (uint32_t it = 0;; ++it) {
+    const int seen = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (seen >= v) return seen;
     if (it >= kSplitSpinLimit) {
       atomicAdd(&g_ouz_split_timeouts, 1u);
-      break;
+      return v;
     }
     __builtin_amdgcn_s_sleep(1);
   }
@@ -112,6 +116,7 @@ __device__ __forceinline__ void pv_split_correct(const SplitLane& sl, PvReal x[9
 __device__ __forceinline__ void pv_cov_split(SplitPvLds& L, int k, uint32_t lane, float pf[45], float dt,
                                              bool pos_fix, bool vel_fix) {
   split_wait(&L.att_count, k + 1);
+  if (kStampSlots > 13 && k == 8) OUZ_STAMP(30, false);
   const float4 o = L.att[k][lane];
   PvReal P[45];
 #pragma unroll
@@ -142,6 +147,7 @@ __device__ __forceinline__ void pv_cov_split(SplitPvLds& L, int k, uint32_t lane
   }
 #pragma unroll
   for (int f = 0; f < 45; ++f) pf[f] = (float)P[f];
+  if (kStampSlots > 13 && k == 8) OUZ_STAMP(31, false);
 }
 
 }  // namespace ouz
