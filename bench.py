@@ -241,9 +241,10 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
     else:
         b = BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES
     achieved = b * n / (us_per_step * 1e-6) / 1e9
-    # a streamed rollout's launches are step kernels writing a storage row instead of the env buffers (the same
-    # bytes): priced with the step kernel's PMC summary
-    traffic = load_traffic("step" if streamed else kernel, task, n)
+    # a streamed rollout's launches are step kernels writing a storage row instead of the env buffers: priced with
+    # the summary of that workload itself (scripts/gpu_roofline_evidence.sh rollout entries; the step-mode
+    # launches, which rewrite the same env buffers every step, run ~15 % faster at 4 M envs and would overstate it)
+    traffic = load_traffic(kernel, task, n)
     e = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBPS, 5),
          "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,

@@ -12,10 +12,10 @@ ENTRIES=("$@")
 if [ ${#ENTRIES[@]} -eq 0 ]; then
   for N in 4194304 16777216; do
     for T in LeeLanded QuadTracking QuadFault QuadMixed; do
-      ENTRIES+=("step:$T:$N")
       # the estimator tasks keep the fused rollout at every size; the others stream it through the step
-      # kernel above 131072 envs (bench.py prices those with the step kernel's summary)
-      case $T in QuadTracking|QuadMixed) ENTRIES+=("rollout:$T:$N");; esac
+      # kernel above 131072 envs (one step launch per step into the storage rows: its own entry, since those
+      # launches are not the step-mode ones)
+      ENTRIES+=("step:$T:$N" "rollout:$T:$N")
     done
   done
 fi
