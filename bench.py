@@ -103,7 +103,22 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=24.0, help="total budget of the CPU baseline leg")
     ap.add_argument("--allreduce-batch", type=int, default=8,
                     help="16-step rollouts whose return statistics share one all-reduce (N > 1)")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="side file of the full record (every roofline entry with its traffic detail, the sweep, "
+                         "the CPU table); the stdout line stays compact and names it")
     return ap.parse_args()
+
+
+ESTIMATOR_TASKS = ("EKFLeeLanded", "QuadTracking", "QuadMixed")
+
+
+def task_dtype(task):
+    """The arithmetic types the step computes in, against the reference's: the estimator's EKF runs in f32 where
+    the reference's is numpy f64 (ahrs_ekf.py:1280-1337), its PV filter in f64 registers where the reference's
+    is torch f32 (PVFilter.py:25-110)."""
+    if task in ESTIMATOR_TASKS:
+        return "f32; EKF f32 (reference numpy f64), PV f64 (reference torch f32)"
+    return "f32"
 
 
 # ----------------------------------------------------------------------------------------- CPU baseline
@@ -275,16 +290,20 @@ class HipEvents:
     stream.  torch.cuda.Event.record() costs ~5 us of host time against ~1.5 us for the raw call
     (scripts/exp/event_record_cost.py), and the start event's host time is inside the timed region."""
 
-    LIB = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    @staticmethod
+    def runtime():
+        """The libamdhip64 torch already mapped (never a second copy: distributed.loaded_library)."""
+        from ouzelum_amd.distributed import loaded_library
+        return loaded_library("libamdhip64.so")
 
     @classmethod
     def available(cls):
-        return os.path.exists(cls.LIB)
+        return cls.runtime() is not None
 
     def __init__(self, dev):
         import ctypes
         self._ct = ctypes
-        self.hip = ctypes.CDLL(self.LIB)
+        self.hip = ctypes.CDLL(self.runtime(), mode=getattr(os, "RTLD_NOLOAD", 4) | ctypes.RTLD_GLOBAL)
         self.ev = [ctypes.c_void_p(), ctypes.c_void_p()]
         for e in self.ev:
             if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
@@ -483,7 +502,7 @@ def config_entry(letter, task, n, res, run, sweep=None):
     e = {"config": letter, "task": task, "num_envs_per_gpu": n, "value": round(res["value"], 1),
          "unit": "env-steps/s", "ms_per_step": round(res["ms_per_step"], 5),
          # the PV filter's covariance step runs in f64, the rest of the step in f32
-         "dtype": "f32 + f64 PV" if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else "f32",
+         "dtype": task_dtype(task),
          "roofline": {**roofline_entry("rollout", task, n, res["kernel_us"], RING),
                       "kernel_us_source": "HIP events on the step stream around the timed region / steps",
                       "kernel_us_back_to_back": round(us_b2b, 3)}}
@@ -497,24 +516,160 @@ def config_entry(letter, task, n, res, run, sweep=None):
     return e
 
 
+# ----------------------------------------------------------------------------------------- launcher
+def spawn_ranks(args):
+    """``bench.py --gpus N`` without torchrun: start the N ranks here, one child process per GPU with the
+    variables torchrun would set (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*; the reference launches its
+    multi-GPU path under torchrun, train.py:74-82).  This parent never touches the GPU; rank 0 prints the line.
+    Returns the exit code: non-zero if any rank failed (the others are then stopped)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OUZ_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:   # the exact children started above, never a pattern
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+# ----------------------------------------------------------------------------------------- output
+LINE_LIMIT = 6000   # the stdout line stays well under what the driver parses (BENCH_r03's 26 KB line was not)
+_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "frac_from_rocprof_avg", "kernel",
+              "steps_per_launch", "num_envs", "bytes_per_env_step", "kernel_us", "kernel_us_back_to_back")
+
+
+def compact_roofline(e):
+    """The judged fields of a roofline entry: the PMC traffic stays as bytes per launch, its per-env-step form
+    and evidence path are kept, the rest of the traffic detail goes to the side file."""
+    out = {k: e[k] for k in _ROOF_KEYS if k in e}
+    td = e.get("traffic_detail") or {}
+    if td.get("bytes_per_env_step") is not None:
+        out["traffic_per_env_step"] = td["bytes_per_env_step"]
+    if td.get("rocprof_stats"):
+        out["rocprof_stats"] = td["rocprof_stats"]
+    if td.get("stale"):
+        out["traffic_stale"] = True
+    if e.get("issue"):
+        iss = e["issue"]
+        out["issue"] = {k: iss[k] for k in ("bound", "valu_issue_frac", "simd_frac", "chip_valu_frac",
+                                           "kernel_us_from_counters", "source") if k in iss}
+    return out
+
+
+def compact_line(out):
+    """The one stdout line: headline, its roofline, the per-step path, one row per config, the large-N
+    fractions and the CPU baseline summary.  Everything else is in the side file ``out['detail']``."""
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config") if k in out}
+    line["roofline"] = compact_roofline(out["roofline"])
+    ps = out.get("per_step_launch")
+    if ps:
+        line["per_step_launch"] = {"value": ps["value"], "ms_per_step": ps["ms_per_step"],
+                                   "kernel_us": ps["roofline"].get("kernel_us"), "frac": ps["roofline"].get("frac"),
+                                   "traffic_per_env_step": (ps["roofline"].get("traffic_detail") or {}).get(
+                                       "bytes_per_env_step")}
+    rows = []
+    for c in out.get("configs", []):
+        rf = c["roofline"]
+        row = {"config": c["config"], "task": c["task"], "num_envs": c["num_envs_per_gpu"], "value": c["value"],
+               "ms_per_step": c["ms_per_step"], "dtype": c["dtype"], "frac": rf.get("frac"),
+               "frac_from_rocprof_avg": rf.get("frac_from_rocprof_avg")}
+        if c.get("per_step_launch"):
+            row["per_step_kernel_us"] = c["per_step_launch"]["roofline"].get("kernel_us")
+        if rf.get("issue"):
+            row["valu_issue_frac"] = rf["issue"].get("valu_issue_frac")
+        rows.append(row)
+    if rows:
+        line["configs"] = rows
+    large = {}
+    for task, entries in [(out["config"]["task"], out.get("roofline_sweep") or [])] + [
+            (c["task"], c.get("roofline_sweep") or []) for c in out.get("configs", [])]:
+        for e in entries:
+            kind = "rollout" if e["kernel"] == "quad_rollout_kernel" or e.get("steps_per_rollout") else "step"
+            large[f"{task}/{kind}/{e['num_envs']}"] = {"frac": e.get("frac"),
+                                                       "frac_from_rocprof_avg": e.get("frac_from_rocprof_avg")}
+    if large:
+        line["large_n"] = large
+    cpu = out.get("cpu_baseline")
+    if cpu:
+        c = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cpu}
+        c["by_config"] = {f"{r['config']}/{r['task']}/{r['num_envs']}": r["value"] for r in cpu.get("table", [])}
+        if cpu.get("f32_host"):
+            c["f32_host"] = {f"{r['config']}/{r['task']}/{r['num_envs']}": r["value"] for r in cpu["f32_host"]}
+        line["cpu_baseline"] = c
+    for k in ("split_timeouts", "detail"):
+        if k in out:
+            line[k] = out[k]
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_LIMIT:   # never: drop the least important parts rather than print an unparseable line
+        for k in ("large_n", "configs"):
+            line.pop(k, None)
+            s = json.dumps(line, separators=(",", ":"))
+            if len(s) <= LINE_LIMIT:
+                break
+    return s
+
+
+def write_detail(path, out):
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    with open(path, "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+def split_timeouts():
+    """Give-ups of the split-wave / output-wave LDS waits since the process started (quad_pv_split.h): 0 unless
+    the protocol is broken, in which case the measured rollouts were wrong."""
+    from ouzelum_amd import _lib
+    import ctypes
+    v = ctypes.c_uint32(0)
+    _lib.check(_lib.lib.ouz_split_timeouts(ctypes.byref(v), 0), "ouz_split_timeouts")
+    return int(v.value)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     cpu = None
     if world == 1 and not args.no_cpu_baseline:   # forked workers: before anything initialises the GPU
         cpu = cpu_baseline_leg(args.task, args.num_envs, args.seed, args.cpu_seconds)
 
-    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env
+    from ouzelum_amd.distributed import ReturnAllReduce, init_from_env, rccl_comm_count
     rank, world, local = init_from_env()
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but {world} rank(s) joined", file=sys.stderr)
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+        sys.exit(3)
     # one GPU per rank (torchrun's LOCAL_RANK); modulo the device count so an N-rank rehearsal with
     # OUZ_DIST_BACKEND=gloo can share one GPU
     n_dev = max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local % n_dev)
     torch.cuda.set_device(dev)
     n = args.num_envs
+    comm_count = rccl_comm_count(dev) if world > 1 else None
 
     # per-rollout return statistics all-reduced (RCCL when N > 1) asynchronously on the collective's
     # stream, double-buffered so the next rollouts' steps do not wait for it, and ARB rollouts' rows per
@@ -537,13 +692,18 @@ def main():
     out = {
         "metric": METRIC, "value": round(res["value"], 1), "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(res["ms_per_step"], 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": task_dtype(args.task),
+        "data": "synthetic",
         "config": {"workload": f"config {letter}: {n}-env {desc} ({args.task}), dt 0.01 x 2 sub-steps; "
                                f"16-step rollouts, one persistent launch each (ouz_rollout_stats)",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
-                   "parallelism": f"env-sharded dp{world} (per-16-step-rollout return statistics, async RCCL "
-                                  f"all-reduce of {args.allreduce_batch} rollouts' rows per collective)",
-                   "physical_devices": min(world, n_dev), "backend": backend,
+                   "parallelism": f"env-sharded dp{world} (per-16-step-rollout return statistics, async "
+                                  f"{'RCCL' if backend == 'nccl' else backend or 'no'} all-reduce of "
+                                  f"{args.allreduce_batch} rollouts' rows per collective)",
+                   "ranks_joined": world, "physical_devices": min(world, n_dev), "backend": backend,
+                   "collective": red.collective if world > 1 else None, "rccl_comm_count": comm_count,
+                   "launcher": "bench.py" if os.environ.get("OUZ_BENCH_SPAWNED") else (
+                       "torchrun" if world > 1 else None),
                    "rehearsal": bool(world > 1 and (backend != "nccl" or n_dev < world))},
         "roofline": {**roofline_entry("rollout", args.task, n, res["kernel_us"], RING),
                      "kernel_us_source": "HIP events on the step stream around the timed region / steps "
@@ -577,10 +737,23 @@ def main():
             out["configs"] = cfgs
         if cpu is not None:
             out["cpu_baseline"] = cpu
-    print(json.dumps(out), flush=True)
+    torch.cuda.synchronize(dev)
+    out["split_timeouts"] = split_timeouts()
+    out["detail"] = args.detail
+    try:
+        write_detail(args.detail, out)
+    except OSError as e:   # the line still prints; the side file is a convenience
+        print(f"bench: could not write {args.detail}: {e}", file=sys.stderr)
+        out["detail"] = None
+    print(compact_line(out), flush=True)
+    if out["split_timeouts"]:
+        print(f"bench: {out['split_timeouts']} split-wave waits gave up: the rollouts measured were wrong",
+              file=sys.stderr)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if out["split_timeouts"]:
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -238,6 +238,9 @@ uint32_t ouz_build_flags(void);
  * after ~70 ms instead of hanging the GPU, since the last reset: 0 unless the protocol is broken (its
  * results are then wrong).  reset != 0 zeroes the counter after reading it.  Synchronous. */
 int ouz_split_timeouts(uint32_t* out, int32_t reset);
+/* Test-only: polls before a split-wave / output-wave wait gives up (0 restores the default, ~70 ms).  A small
+ * value forces give-ups, so a test can check that they are reported (QuadVecTask.check_health raises). */
+int ouz_set_split_spin_limit(uint32_t polls);
 /* State slots of a task at num_envs (see "State slots" above); negative on bad arguments. */
 int64_t ouz_state_slots(int32_t task, int32_t num_envs);
 /* State slot of each of num_envs envs of a shard starting at global id env_id_offset, into the host

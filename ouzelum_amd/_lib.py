@@ -23,6 +23,7 @@ class OuzelumError(RuntimeError):
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
 ABI_VERSION = 3
+LAYOUT_VERSION = 3  # the ABI version whose state-slot rules (include/ouzelum.h "State slots") the layout follows
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
@@ -86,6 +87,7 @@ SIGNATURES = {
     "ouz_abi_version": (_I, []),
     "ouz_build_flags": (_U32, []),
     "ouz_split_timeouts": (_I, [_P, _I]),
+    "ouz_set_split_spin_limit": (_I, [_U32]),
     "ouz_state_slots": (_I64, [_I, _I]),
     "ouz_env_slots": (_I, [_I, _I, _I64, _P]),
     "ouz_last_error": (ctypes.c_char_p, []),

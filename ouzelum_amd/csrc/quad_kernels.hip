@@ -2111,6 +2111,12 @@ int ouz_split_timeouts(uint32_t* out, int32_t reset) {
                    "hipMemcpyToSymbol(split timeouts)");
 }
 
+int ouz_set_split_spin_limit(uint32_t polls) {
+  const uint32_t v = polls ? polls : kSplitSpinLimit;
+  return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_ouz_split_spin_limit), &v, sizeof(uint32_t)),
+                   "hipMemcpyToSymbol(split spin limit)");
+}
+
 #ifdef OUZ_STAMPS
 int ouz_probe_stamps(uint64_t* host, int32_t count) {
   const int n = count < kStampWaves * kStampSlots ? count : kStampWaves * kStampSlots;

@@ -20,8 +20,10 @@
 // wave publishes step k's attitude before it can wait for step k's gains; the covariance wave publishes those
 // gains right after computing them from that attitude), both waves of the workgroup are resident together, and
 // both run the same K steps with the same wave-uniform fix decisions.  A wait that still exceeds
-// kSplitSpinLimit polls (~70 ms) gives up, counts itself in g_ouz_split_timeouts (ouz_split_timeouts) and lets
-// the launch drain: a protocol error shows up as a count and wrong results, never as a hung GPU.
+// g_ouz_split_spin_limit polls (kSplitSpinLimit, ~70 ms, unless a test lowers it with ouz_set_split_spin_limit)
+// gives up, counts itself in g_ouz_split_timeouts (ouz_split_timeouts) and lets the launch drain: a protocol error
+// shows up as a count, never as a hung GPU.  The count is not silent: QuadVecTask reads it at its synchronisation
+// points (check_health) and raises, and bench.py records it and fails on a non-zero count.
 #pragma once
 #include "quad_math.h"
 
@@ -31,6 +33,7 @@ constexpr int kSplitRing = 32;                  // attitude slots: one per step 
 constexpr uint32_t kSplitSpinLimit = 1u << 20;  // polls of ~64 cycles before a wait gives up
 
 __device__ uint32_t g_ouz_split_timeouts;
+__device__ uint32_t g_ouz_split_spin_limit = kSplitSpinLimit;
 
 struct SplitPvLds {
   float4 att[kSplitRing][64];   // [step][lane] the quaternion (w, x, y, z) the PV step of that step uses
@@ -54,7 +57,7 @@ __device__ __forceinline__ int split_wait(int* f, int v) {
   for (uint32_t it = 0;; ++it) {
     const int seen = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (seen >= v) return seen;
-    if (it >= kSplitSpinLimit) {
+    if (it >= g_ouz_split_spin_limit) {
       atomicAdd(&g_ouz_split_timeouts, 1u);
       return v;
     }

@@ -32,6 +32,56 @@ def init_from_env(backend=None):
     return rank, world, local
 
 
+def loaded_library(stem):
+    """Path of a shared library this process has ALREADY mapped whose file name starts with ``stem`` (e.g.
+    "libamdhip64.so", "librccl.so"), from /proc/self/maps, or None.  The direct collectives and the bench's raw
+    events call into the runtime torch itself loaded: opening another copy by path (torch/lib against
+    /opt/rocm/lib) would give a second HIP / RCCL runtime, whose calls on torch's streams and communicator
+    crash instead of failing."""
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                parts = line.split()
+                if len(parts) >= 6 and os.path.basename(parts[5]).startswith(stem):
+                    return parts[5]
+    except OSError:  # pragma: no cover - not Linux
+        return None
+    return None
+
+
+def _comm_ptr(dev):
+    """The ncclComm_t of the default process group's RCCL backend on ``dev`` (0 if unavailable).  This goes
+    through torch's private ProcessGroup API (``_get_backend(dev)._comm_ptr()``, present in torch 2.4-2.10);
+    any other torch raises AttributeError / RuntimeError here and the callers fall back."""
+    grp = dist.distributed_c10d._get_default_group()
+    be = grp._get_backend(dev)
+    fn = getattr(be, "_comm_ptr", None)
+    if fn is None:
+        raise AttributeError(f"torch {torch.__version__}: ProcessGroupNCCL has no _comm_ptr()")
+    return int(fn())
+
+
+def rccl_comm_count(dev):
+    """Ranks of the RCCL communicator the process group runs its collectives on (``ncclCommCount``), or None
+    when the backend is not RCCL or the communicator cannot be reached."""
+    import ctypes
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend() != dist.Backend.NCCL:
+        return None
+    try:
+        comm = _comm_ptr(dev)
+        path = loaded_library("librccl.so")
+        if not comm or not path:
+            return None
+        rccl = ctypes.CDLL(path, mode=getattr(os, "RTLD_NOLOAD", 4) | ctypes.RTLD_GLOBAL)
+        cnt = ctypes.c_int(0)
+        rccl.ncclCommCount.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        if rccl.ncclCommCount(ctypes.c_void_p(comm), ctypes.byref(cnt)) != 0:
+            return None
+        return int(cnt.value)
+    except Exception:  # noqa: BLE001 -- a report field, never a reason to fail the run
+        return None
+
+
 def shard(num_envs_local, rank, world):
     """(env_id_offset, num_envs_total) for this rank."""
     return rank * num_envs_local, world * num_envs_local
@@ -62,14 +112,17 @@ class DirectCollectives:
     whatever stream they are on.
     """
 
-    LIB = os.path.join(os.path.dirname(torch.__file__), "lib")
-    NCCL_FLOAT64, NCCL_SUM = 8, 0
+    NCCL_FLOAT64, NCCL_SUM = 8, 0   # ncclDataType_t / ncclRedOp_t values of nccl.h (RCCL keeps NCCL's enums)
 
     def __init__(self, slots):
         import ctypes
         self._ct = ctypes
-        self.hip = ctypes.CDLL(os.path.join(self.LIB, "libamdhip64.so"))
-        self.rccl = ctypes.CDLL(os.path.join(self.LIB, "librccl.so"))
+        hip_path, rccl_path = loaded_library("libamdhip64.so"), loaded_library("librccl.so")
+        if not hip_path or not rccl_path:
+            raise RuntimeError("the HIP / RCCL runtimes torch loaded are not mapped in this process")
+        noload = getattr(os, "RTLD_NOLOAD", 4)
+        self.hip = ctypes.CDLL(hip_path, mode=noload | ctypes.RTLD_GLOBAL)
+        self.rccl = ctypes.CDLL(rccl_path, mode=noload | ctypes.RTLD_GLOBAL)
         self.rccl.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         self.rccl.ncclAllReduce.restype = ctypes.c_int
@@ -77,8 +130,7 @@ class DirectCollectives:
         self._dev = dev
         self.cs = torch.cuda.Stream(device=dev)
         self._cs = ctypes.c_void_p(self.cs.cuda_stream)
-        pg = dist.distributed_c10d._get_default_group()._get_backend(dev)
-        comm = pg._comm_ptr()
+        comm = _comm_ptr(dev)
         if not comm:
             raise RuntimeError("the process group has no RCCL communicator")
         self._comm = ctypes.c_void_p(comm)
@@ -146,11 +198,12 @@ class ReturnAllReduce:
     its last row is submitted, on the collective's own stream while the next rollouts step.  One
     eager call of ``dist.all_reduce`` costs 13-22 us of host time (RCCL, ``profiles/r01/allreduce_host.txt``,
     ``profiles/r03/allreduce_host.jsonl``), as much as five 4096-env steps, so ``batch`` rollouts
-    share it; the per-rollout global statistics are unchanged.  ``collective="direct"`` (the default on
-    the "nccl" backend, i.e. RCCL) issues the same collectives as direct RCCL calls on the process group's
-    communicator instead (``DirectCollectives``, about half the host time per flush); it is checked at
-    construction on every rank and falls back to eager, on all ranks together, if the check fails.
-    ``OUZ_COLLECTIVE=eager`` forces the eager form.  A block is only reused after its
+    share it; the per-rollout global statistics are unchanged.  ``collective="direct"`` (opt-in on the
+    "nccl" backend, i.e. RCCL, with ``OUZ_COLLECTIVE=direct``) issues the same collectives as direct RCCL calls
+    on the process group's communicator instead (``DirectCollectives``, about half the host time per flush); it
+    is checked at construction on every rank and falls back to eager, on all ranks together, if the check
+    fails.  The default is ``eager`` (``dist.all_reduce``): the direct form has only run on a one-rank RCCL
+    communicator, and until a run on two or more GPUs validates it, the product path uses torch's own.  A block is only reused after its
     collectives have completed (``wait`` orders the current stream after them).  ``result(r)``
     returns the global [sum, count, ...] of rollout r, flushing the rows not yet reduced first;
     every rank must make the same calls in the same order (they are collectives).
@@ -169,7 +222,7 @@ class ReturnAllReduce:
         self._row_bytes = width * self.slots.element_size()
         self.direct = None
         if collective is None:
-            collective = os.environ.get("OUZ_COLLECTIVE", "direct")
+            collective = os.environ.get("OUZ_COLLECTIVE", "eager")
         if collective not in ("direct", "eager"):
             raise ValueError(f"collective must be 'direct' or 'eager', not {collective!r}")
         if (self.active and collective == "direct" and self.slots.is_cuda

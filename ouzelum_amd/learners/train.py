@@ -109,6 +109,7 @@ def train(args):
             dist.all_reduce(mean_rew)
             mean_rew /= world
         torch.cuda.synchronize(device)
+        base.check_health()   # raises if a fused rollout's split-wave wait gave up (never on the per-step path)
         sps = N * world * T / (time.perf_counter() - t0)
         row = {"global_step": global_step, "average_reward": float(mean_rew), "episodes": int(ep[1]),
                "episodic_return": float(ep[0] / ep[1]) if float(ep[1]) > 0 else float("nan"),

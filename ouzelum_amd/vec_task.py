@@ -275,9 +275,23 @@ class QuadVecTask:
 
     def landings(self) -> int:
         """Total landings over all finished episodes (ekf_lee_landed.py:319-331 'Landoa')."""
-        return int(self.istate[:, L.I_LANDINGS].sum().item())
+        n = int(self.istate[:, L.I_LANDINGS].sum().item())
+        self.check_health()
+        return n
 
-    def episode_stats(self, drain=True, out=None):
+    def check_health(self):
+        """Raise ``OuzelumError`` if a split-wave / output-wave LDS wait of a fused rollout gave up since the last
+        check (``ouz_split_timeouts``; quad_pv_split.h): the rollout then drained with wrong results, and nothing
+        computed from it may be used.  Synchronous (it reads a device counter), so it runs where the env already
+        synchronises: ``state_dict`` / ``load_state_dict``, ``landings``, ``trace_since``, ``rollout(check=True)``,
+        ``episode_stats(check=True)``, and the learners' per-update logging."""
+        v = ctypes.c_uint32(0)
+        L.check(L.lib.ouz_split_timeouts(ctypes.byref(v), 1), "ouz_split_timeouts")
+        if v.value:
+            raise L.OuzelumError(f"{v.value} split-wave wait(s) of a fused rollout gave up (a broken LDS protocol "
+                                 "or a stalled partner wave): the rollouts since the last check are wrong")
+
+    def episode_stats(self, drain=True, out=None, check=False):
         """[sum of returns, count, sum of lengths] of episodes finished since the last drain, as a
         float64 device tensor — the quantities RecordEpisodeStatisticsTorch reports as info["r"] /
         info["l"] (PPO/utils.py:20-35); config E all-reduces it over RCCL.  One kernel
@@ -293,6 +307,9 @@ class QuadVecTask:
             raise ValueError("episode_stats: out must be a contiguous float64 tensor of >= 3 on the env device")
         L.check(L.lib.ouz_episode_stats(self._env, L.ptr(buf), 1 if drain else 0, self._stream()),
                 "ouz_episode_stats")
+        if check:
+            torch.cuda.synchronize(self.device)
+            self.check_health()
         return buf
 
     _DRN_DIST = {"gaussian": 1, "uniform": 2}
@@ -346,6 +363,7 @@ class QuadVecTask:
         if now - step > cap:
             raise RuntimeError(f"trace overrun: {now - step} steps since {step}, capacity {cap}")
         torch.cuda.synchronize(self.device)
+        self.check_health()
         steps = np.arange(step, now)
         idx = torch.as_tensor(steps % cap, device=self.device)
         return steps, tr[idx].cpu().numpy(), rs[idx].cpu().numpy().astype(np.int64)
@@ -381,7 +399,7 @@ class QuadVecTask:
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
 
-    def rollout(self, action_ring, n_steps, fused=False, storage=None, stats_out=None, drain=True):
+    def rollout(self, action_ring, n_steps, fused=False, storage=None, stats_out=None, drain=True, check=False):
         """``n_steps`` consecutive VecTask.step calls over a ring of pre-staged action batches
         ``(T, N, 4)`` (``None`` for the Lee tasks, which ignore actions) with one C call.
 
@@ -396,8 +414,15 @@ class QuadVecTask:
         step's outputs land in the learner's rollout buffers, the env buffers keep the last step.
         ``stats_out`` (a float64 device tensor of >= 3): also write the episode statistics after
         the last step, as ``episode_stats(drain, out=stats_out)`` would (``ouz_step_n_stats``: one
-        host call for the steps and the statistics).
+        host call for the steps and the statistics).  ``check``: synchronise after the launches and
+        ``check_health()`` (raises if a split-wave wait of these rollouts gave up).
         """
+        self._rollout(action_ring, n_steps, fused, storage, stats_out, drain)
+        if check:
+            torch.cuda.synchronize(self.device)
+            self.check_health()
+
+    def _rollout(self, action_ring, n_steps, fused, storage, stats_out, drain):
         if stats_out is not None:
             if not self.cfg.track_episodes:
                 raise RuntimeError("create the env with track_episodes=True")
@@ -504,20 +529,36 @@ class QuadVecTask:
     def _layout(self):
         """What fixes the slot order of fstate / istate: the ABI's layout rules, the slot count and the shard's
         place among the global ids (the mixed curriculum's slot map depends on env_id_offset)."""
-        return {"abi": L.ABI_VERSION, "slots": int(self.fstate.shape[0]) * L.TILE,
+        return {"abi": L.LAYOUT_VERSION, "slots": int(self.fstate.shape[0]) * L.TILE,
                 "env_id_offset": int(self.cfg.env_id_offset), "num_envs_total": int(self.cfg.num_envs_total)}
 
     def state_dict(self):
         """Env-state checkpoint (the reference never checkpoints env state).  The state is saved in
-        slot order together with its layout marker; ``load_state_dict`` refuses a checkpoint of another layout."""
+        slot order together with its layout marker; ``load_state_dict`` refuses a checkpoint of another layout.
+        Raises (``check_health``) if a fused rollout since the last check gave up a split-wave wait."""
+        torch.cuda.synchronize(self.device)
+        self.check_health()
         return {"fstate": self.fstate.clone(), "istate": self.istate.clone(), "obs": self.obs_buf.clone(),
                 "rew": self.rew_buf.clone(), "reset": self.reset_buf.clone(), "timeouts": self.timeout_buf.clone(),
                 "step": self.sim_step_count, "task": self.task, "num_envs": self.num_envs, "layout": self._layout()}
 
-    def load_state_dict(self, sd):
+    def load_state_dict(self, sd, strict=True):
+        """Restore a ``state_dict``.  A checkpoint whose layout marker differs from this env's is refused (its slot
+        order differs: ABI version, slot count or shard offset).  A checkpoint written before the marker existed
+        (no ``layout`` key) is loaded with a warning when its tensor shapes match, or refused if ``strict`` and
+        the shapes do not; ``strict=False`` skips the layout comparison altogether (the caller vouches for it)."""
+        import warnings
         if sd["task"] != self.task or sd["num_envs"] != self.num_envs:
             raise ValueError("checkpoint is for a different task / env count")
-        if sd.get("layout") != self._layout():
+        shapes_match = (tuple(sd["fstate"].shape) == tuple(self.fstate.shape)
+                        and tuple(sd["istate"].shape) == tuple(self.istate.shape))
+        if not shapes_match:
+            raise ValueError(f"checkpoint state shapes {tuple(sd['fstate'].shape)} / {tuple(sd['istate'].shape)} != "
+                             f"this env's {tuple(self.fstate.shape)} / {tuple(self.istate.shape)}")
+        if "layout" not in sd:
+            warnings.warn("env checkpoint without a layout marker (written before ABI 3's marker): loaded because "
+                          "its shapes match; its slot order is assumed to be this env's", stacklevel=2)
+        elif strict and sd["layout"] != self._layout():
             raise ValueError(f"checkpoint state layout {sd.get('layout')} != this env's {self._layout()} "
                              "(slot order differs: ABI version, slot count or shard offset)")
         self.fstate.copy_(sd["fstate"])

@@ -36,7 +36,7 @@ def _free_port():
 
 
 def test_direct_collectives_on_rccl():
-    """The direct-RCCL form of ReturnAllReduce's collectives (DirectCollectives, the default on RCCL at N > 1) on
+    """The direct-RCCL form of ReturnAllReduce's collectives (DirectCollectives, opt-in with OUZ_COLLECTIVE=direct) on
     a one-rank RCCL group: set-up on the process group's communicator, the construction-time check, and every
     row range of both blocks flushed and waited for."""
     if not torch.cuda.is_available():
