@@ -15,6 +15,9 @@ import torch  # noqa: F401  -- load torch's HIP runtime first so ours binds to t
 LIB_NAME = "libouzelum_hip.so"
 # OUZ_LIB: an alternative in-tree build (probe builds of scripts/; never the product default)
 LIB_PATH = os.environ.get("OUZ_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# the host build of the same step (include/ouzelum_host.h): make(sim_device="cpu")
+HOST_LIB_NAME = "libouzelum_cpu.so"
+HOST_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), HOST_LIB_NAME)
 
 
 class OuzelumError(RuntimeError):
@@ -124,6 +127,58 @@ SIGNATURES = {
     "ouz_lstm_cell_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ouz_lstm_cell_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
 }
+
+
+# include/ouzelum_host.h, the same way: this table IS the list of symbols that header declares.
+HOST_SIGNATURES = {
+    "ouz_host_abi_version": (_I, []),
+    "ouz_host_last_error": (ctypes.c_char_p, []),
+    "ouz_host_create": (_I, [ctypes.POINTER(OuzConfig), ctypes.POINTER(_P)]),
+    "ouz_host_destroy": (_I, [_P]),
+    "ouz_host_bind": (_I, [_P, ctypes.POINTER(OuzBuffers)]),
+    "ouz_host_set_threads": (_I, [_P, _I]),
+    "ouz_host_init_state": (_I, [_P]),
+    "ouz_host_step": (_I, [_P, _P]),
+    "ouz_host_step_n": (_I, [_P, _P, _I, _I]),
+    "ouz_host_reset_idx": (_I, [_P, _P, _I]),
+    "ouz_host_reset_all": (_I, [_P]),
+    "ouz_host_episode_stats": (_I, [_P, _P, _I]),
+    "ouz_host_set_trace": (_I, [_P, _P, _P, _I, _I]),
+    "ouz_host_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
+    "ouz_host_get_step": (_I64, [_P]),
+    "ouz_host_set_step": (_I, [_P, _I64]),
+}
+
+_hostlib = None
+
+
+def host_lib():
+    """``libouzelum_cpu.so`` (loaded on first use: only make(sim_device="cpu") needs it)."""
+    global _hostlib
+    if _hostlib is None:
+        if not os.path.exists(HOST_LIB_PATH):
+            raise OuzelumError(f"{HOST_LIB_NAME} not found at {HOST_LIB_PATH}: build it first "
+                               "(python -m ouzelum_amd.build)")
+        try:
+            h = ctypes.CDLL(HOST_LIB_PATH)
+        except OSError as e:  # pragma: no cover - depends on the machine
+            raise OuzelumError(f"failed to load {HOST_LIB_PATH}: {e}") from e
+        for name, (res, args) in HOST_SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        if h.ouz_host_abi_version() != ABI_VERSION:
+            raise OuzelumError(f"ABI mismatch: host library {h.ouz_host_abi_version()} != binding {ABI_VERSION}")
+        _hostlib = h
+    return _hostlib
+
+
+def host_check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = host_lib().ouz_host_last_error().decode(errors="replace")
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        raise OuzelumError(f"{what} failed ({rc}): {msg}")
 
 
 def _load():

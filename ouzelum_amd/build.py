@@ -10,8 +10,20 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRCS = [os.path.join(HERE, "csrc", "quad_kernels.hip"), os.path.join(HERE, "csrc", "learner_kernels.hip")]
-DEPS = [*SRCS, *(os.path.join(HERE, "csrc", h) for h in ("quad_math.h", "philox.h", "quad_pv_ql.h", "quad_pv_split.h")),
+DEPS = [*SRCS, *(os.path.join(HERE, "csrc", h) for h in ("quad_math.h", "quad_env.h", "philox.h", "quad_pv_ql.h",
+                                                          "quad_pv_split.h")),
         os.path.join(ROOT, "include", "ouzelum.h")]
+# the host build of the same step (make(sim_device="cpu"); include/ouzelum_host.h)
+HOST_SRC = os.path.join(HERE, "csrc", "quad_host.cpp")
+HOST_DEPS = [HOST_SRC, *(os.path.join(HERE, "csrc", h) for h in ("quad_math.h", "quad_env.h", "philox.h",
+                                                                 "host_compat.h")),
+             os.path.join(ROOT, "include", "ouzelum.h"), os.path.join(ROOT, "include", "ouzelum_host.h")]
+HOST_OUT = os.path.join(HERE, "libouzelum_cpu.so")
+CXX = os.environ.get("CXX", "g++")
+# x86-64-v3 (AVX2 + FMA): the build container's and the GPU boxes' EPYC hosts; no FMA contraction (the f32 step
+# rounds each operation, like the oracle's numpy), OpenMP over the envs of a step (libgomp, torch's own runtime)
+HOST_FLAGS = ["-O3", "-std=c++17", "-march=x86-64-v3", "-ffp-contract=off", "-fopenmp", "-fPIC", "-shared",
+              "-Wall", "-Wno-unknown-pragmas", "-Wno-unused-variable", "-DOUZ_HOST"]
 OUT = os.environ.get("OUZ_BUILD_OUT") or os.path.join(HERE, "libouzelum_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("OUZ_OFFLOAD_ARCH", "gfx950")
@@ -43,14 +55,27 @@ FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wn
          "-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 
 
-def up_to_date() -> bool:
-    if not os.path.exists(OUT):
+def up_to_date(out=OUT, deps=DEPS) -> bool:
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(d) <= t for d in DEPS)
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def build_host(force: bool = False, verbose: bool = True) -> str:
+    """libouzelum_cpu.so: quad_host.cpp (quad_env.h + quad_math.h for the host) with g++ and OpenMP."""
+    if not force and up_to_date(HOST_OUT, HOST_DEPS):
+        return HOST_OUT
+    cmd = [CXX, *HOST_FLAGS, "-o", HOST_OUT + ".tmp", HOST_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(HOST_OUT + ".tmp", HOST_OUT)
+    return HOST_OUT
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
+    build_host(force=force, verbose=verbose)
     if not force and up_to_date():
         return OUT
     extra = os.environ.get("OUZ_EXTRA_FLAGS", "").split()

@@ -10,7 +10,11 @@
 // form is used instead (derivations in DESIGN.md §4); the literal float64 form
 // lives in the CPU oracle, pinned against the reference's own modules.
 #pragma once
+#ifdef OUZ_HOST
+#include "host_compat.h"   // the host build of the step (quad_host.cpp)
+#else
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include <type_traits>

@@ -17,9 +17,15 @@ Mirrors the reference's ``VecTask`` surface that the PPO/RPO learners consume
 One ``step`` is ONE kernel launch (``ouz_step``) on the current HIP stream with
 no host synchronisation.  Buffers are torch tensors owned here; the C library
 only holds their device pointers.
+
+``sim_device="cpu"`` (the reference's VecTask accepts a CPU device, vec_task.py:169-223) runs the same
+per-env step compiled for the host (``libouzelum_cpu.so``, include/ouzelum_host.h: quad_env.h + quad_math.h
+with OpenMP over envs) on CPU tensors of the same layout; calls are synchronous.  It is a product path of its
+own, not a fallback: a HIP env never routes to it, and it never uses the test oracle.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import numpy as np
@@ -54,7 +60,7 @@ class QuadVecTask:
 
     def __init__(self, task="LeeLanded", num_envs=4096, sim_device="cuda:0", rl_device=None, seed=0,
                  env_id_offset=0, num_envs_total=None, pomdp=None, pomdp_prob=None, clip_obs=5.0,
-                 clip_actions=1.0, track_episodes=False, **overrides):
+                 clip_actions=1.0, track_episodes=False, host_threads=0, **overrides):
         if isinstance(task, str):
             if task not in TASK_IDS:
                 raise ValueError(f"unknown task {task!r}; one of {sorted(TASK_IDS)}")
@@ -67,12 +73,15 @@ class QuadVecTask:
         if clip_obs != 5.0 or clip_actions != 1.0:
             raise ValueError("clipObservations=5 and clipActions=1 are fixed by the kernel (cfg/task/*.yaml)")
         dev = torch.device(sim_device)
-        if dev.type != "cuda":
-            raise L.OuzelumError(f"sim_device {sim_device!r}: the quadrotor step runs only on a HIP device; "
-                                 "there is no CPU pipeline (the CPU restatement lives in oracle/ and is test-only)")
-        if not torch.cuda.is_available():
-            raise L.OuzelumError("no HIP device visible: QuadVecTask needs an MI355X")
-        self.device = dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.type not in ("cuda", "cpu"):
+            raise ValueError(f"sim_device {sim_device!r}: a HIP device (cuda:N) or cpu")
+        self._host = dev.type == "cpu"
+        if self._host:   # the host build of the step (libouzelum_cpu.so)
+            self.device = torch.device("cpu")
+        else:
+            if not torch.cuda.is_available():
+                raise L.OuzelumError("no HIP device visible: QuadVecTask needs an MI355X (or sim_device='cpu')")
+            self.device = dev if dev.index is not None else torch.device("cuda", torch.cuda.current_device())
         self.rl_device = torch.device(rl_device) if rl_device is not None else self.device
         n = int(num_envs)
         cfg = L.OuzConfig()
@@ -82,7 +91,7 @@ class QuadVecTask:
         cfg.env_id_offset = int(env_id_offset)
         cfg.num_envs_total = int(num_envs_total or n)
         cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        cfg.device = self.device.index
+        cfg.device = -1 if self._host else self.device.index
         cfg.pomdp = POMDP_IDS[pomdp]
         cfg.pomdp_prob = -1.0 if pomdp_prob is None else float(pomdp_prob)
         cfg.track_episodes = 1 if track_episodes else 0
@@ -110,7 +119,7 @@ class QuadVecTask:
         self.act_space = Box(np.ones(self.num_actions) * -1.0, np.ones(self.num_actions) * 1.0)
 
         # --- buffers (owned here; allocate_buffers vec_task.py:254-277) ---
-        with torch.cuda.device(self.device):
+        with (contextlib.nullcontext() if self._host else torch.cuda.device(self.device)):
             # wave-tiled SoA [tiles][fields][64] over the task's state slots (include/ouzelum.h "State slots":
             # the estimator tasks group envs by PV trigger class); padding slots stay 0
             slots = int(L.lib.ouz_state_slots(self.task, n))
@@ -130,14 +139,23 @@ class QuadVecTask:
         self.states_buf = torch.zeros((n, 0), dtype=torch.float32, device=self.device)
         self.extras = {}
         self.obs_dict = {}
-        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._dev_index = None if self._host else (
+            self.device.index if self.device.index is not None else torch.cuda.current_device())
         self._act_shape = torch.Size((n, L.NUM_ACT))
 
         handle = ctypes.c_void_p()
-        L.check(L.lib.ouz_create(cfg, handle), "ouz_create")
-        self._env = handle
         bufs = L.OuzBuffers(L.ptr(self.fstate), L.ptr(self.istate), L.ptr(self.obs_buf), L.ptr(self.rew_buf),
                             L.ptr(self.reset_buf), L.ptr(self.timeout_buf))
+        if self._host:
+            H = L.host_lib()
+            L.host_check(H.ouz_host_create(cfg, handle), "ouz_host_create")
+            self._env = handle
+            L.host_check(H.ouz_host_bind(self._env, bufs), "ouz_host_bind")
+            L.host_check(H.ouz_host_set_threads(self._env, int(host_threads)), "ouz_host_set_threads")
+            L.host_check(H.ouz_host_init_state(self._env), "ouz_host_init_state")
+            return
+        L.check(L.lib.ouz_create(cfg, handle), "ouz_create")
+        self._env = handle
         L.check(L.lib.ouz_bind(self._env, bufs), "ouz_bind")
         L.check(L.lib.ouz_init_state(self._env, self._stream()), "ouz_init_state")
 
@@ -145,8 +163,17 @@ class QuadVecTask:
     def _stream(self):
         return L.stream_ptr(self.device)
 
+    def _sync(self):
+        if not self._host:
+            torch.cuda.synchronize(self.device)
+
     def __del__(self):
         env = getattr(self, "_env", None)
+        if env is not None and env.value and getattr(self, "_host", False):
+            if L._hostlib is not None:
+                L._hostlib.ouz_host_destroy(env)
+            self._env = None
+            return
         if env is not None and env.value:
             try:
                 torch.cuda.synchronize(self.device)
@@ -227,6 +254,8 @@ class QuadVecTask:
         It MODIFIES the env state: the lazy reset, thrust integrator, EKF / PV filters and waypoint are written
         back and reset_buf is cleared for the envs it reset, so a following ``step`` with the same step counter
         would run them again.  Save ``state_dict()`` before and load it after if the env is to step on."""
+        if self._host:
+            raise NotImplementedError("pre_physics is a component entry of the HIP path (ouz_pre_physics)")
         wrench = torch.empty((self.num_envs, 6), dtype=torch.float32, device=self.device)
         L.check(L.lib.ouz_pre_physics(self._env, self._actions_ptr(actions), L.ptr(wrench), self._stream()),
                 "ouz_pre_physics")
@@ -271,6 +300,8 @@ class QuadVecTask:
 
     @property
     def sim_step_count(self) -> int:
+        if self._host:
+            return int(L.host_lib().ouz_host_get_step(self._env))
         return int(L.lib.ouz_get_step(self._env))
 
     def landings(self) -> int:
@@ -284,7 +315,9 @@ class QuadVecTask:
         check (``ouz_split_timeouts``; quad_pv_split.h): the rollout then drained with wrong results, and nothing
         computed from it may be used.  Synchronous (it reads a device counter), so it runs where the env already
         synchronises: ``state_dict`` / ``load_state_dict``, ``landings``, ``trace_since``, ``rollout(check=True)``,
-        ``episode_stats(check=True)``, and the learners' per-update logging."""
+        ``episode_stats(check=True)``, and the learners' per-update logging.  The host build has no such waits."""
+        if self._host:
+            return
         v = ctypes.c_uint32(0)
         L.check(L.lib.ouz_split_timeouts(ctypes.byref(v), 1), "ouz_split_timeouts")
         if v.value:
@@ -305,6 +338,10 @@ class QuadVecTask:
         if out is not None and (out.dtype != torch.float64 or out.numel() < 3 or not out.is_contiguous()
                                 or out.device != self.device):
             raise ValueError("episode_stats: out must be a contiguous float64 tensor of >= 3 on the env device")
+        if self._host:
+            L.host_check(L.host_lib().ouz_host_episode_stats(self._env, L.ptr(buf), 1 if drain else 0),
+                         "ouz_host_episode_stats")
+            return buf
         L.check(L.lib.ouz_episode_stats(self._env, L.ptr(buf), 1 if drain else 0, self._stream()),
                 "ouz_episode_stats")
         if check:
@@ -325,6 +362,10 @@ class QuadVecTask:
         if unknown:
             raise NotImplementedError(f"randomization entries {sorted(unknown)} are not implemented on the HIP path")
         for target, key in ((0, "observations"), (1, "actions")):
+            if self._host:
+                L.host_check(L.host_lib().ouz_host_set_dr_noise(self._env, target, self._dr_struct(dr_params.get(key))),
+                             "ouz_host_set_dr_noise")
+                continue
             L.check(L.lib.ouz_set_dr_noise(self._env, target, self._dr_struct(dr_params.get(key))),
                     "ouz_set_dr_noise")
 
@@ -343,13 +384,15 @@ class QuadVecTask:
     def enable_trace(self, env_index=0, capacity=4096):
         """Record (p, target, v) of one env and the number of envs reset at every step, written by
         the step kernel itself (``ouz_set_trace``).  Read with ``trace_since``; see outputs.py."""
+        set_trace = (lambda *a: L.host_check(L.host_lib().ouz_host_set_trace(*a), "ouz_host_set_trace")) \
+            if self._host else (lambda *a: L.check(L.lib.ouz_set_trace(*a), "ouz_set_trace"))
         if capacity == 0:
-            L.check(L.lib.ouz_set_trace(self._env, None, None, 0, 0), "ouz_set_trace")
+            set_trace(self._env, None, None, 0, 0)
             self._trace = None
             return
         tr = torch.zeros((capacity, 9), dtype=torch.float32, device=self.device)
         rs = torch.zeros(capacity, dtype=torch.int32, device=self.device)
-        L.check(L.lib.ouz_set_trace(self._env, L.ptr(tr), L.ptr(rs), int(env_index), int(capacity)), "ouz_set_trace")
+        set_trace(self._env, L.ptr(tr), L.ptr(rs), int(env_index), int(capacity))
         self._trace = (tr, rs, self.sim_step_count)
 
     def trace_since(self, step):
@@ -362,7 +405,7 @@ class QuadVecTask:
         cap = tr.shape[0]
         if now - step > cap:
             raise RuntimeError(f"trace overrun: {now - step} steps since {step}, capacity {cap}")
-        torch.cuda.synchronize(self.device)
+        self._sync()
         self.check_health()
         steps = np.arange(step, now)
         idx = torch.as_tensor(steps % cap, device=self.device)
@@ -374,6 +417,15 @@ class QuadVecTask:
     def _actions_ptr(self, actions):
         if actions is None:
             return L.ptr(self._zero_actions)
+        if self._host:
+            if not isinstance(actions, torch.Tensor):
+                raise TypeError("actions must be a torch tensor")
+            if actions.shape != (self.num_envs, self.num_actions):
+                raise ValueError(f"actions shape {tuple(actions.shape)} != {(self.num_envs, self.num_actions)}")
+            if actions.device.type != "cpu" or actions.dtype != torch.float32 or not actions.is_contiguous():
+                actions = actions.to(device="cpu", dtype=torch.float32).contiguous()
+            self._last_actions = actions
+            return L.ptr(actions)
         # fast path (the learners' case: a contiguous f32 (N, 4) tensor on this device) in a few C calls;
         # everything else goes through the checks and conversion below
         if (type(actions) is torch.Tensor and actions.dtype is torch.float32 and actions.is_cuda
@@ -392,9 +444,12 @@ class QuadVecTask:
 
     def step(self, actions):
         """VecTask.step (vec_task.py:313-359): clamp -> pre -> simulate -> post -> timeouts -> obs clamp."""
-        rc = L.lib.ouz_step(self._env, self._actions_ptr(actions), L.stream_ptr(self._dev_index))
-        if rc:
-            L.check(rc, "ouz_step")
+        if self._host:
+            L.host_check(L.host_lib().ouz_host_step(self._env, self._actions_ptr(actions)), "ouz_host_step")
+        else:
+            rc = L.lib.ouz_step(self._env, self._actions_ptr(actions), L.stream_ptr(self._dev_index))
+            if rc:
+                L.check(rc, "ouz_step")
         self.extras["time_outs"] = self.timeout_buf
         self.obs_dict["obs"] = self.obs_buf
         return self.obs_dict, self.rew_buf, self.reset_buf, self.extras
@@ -417,10 +472,46 @@ class QuadVecTask:
         host call for the steps and the statistics).  ``check``: synchronise after the launches and
         ``check_health()`` (raises if a split-wave wait of these rollouts gave up).
         """
+        if self._host:
+            self._host_rollout(action_ring, n_steps, storage, stats_out, drain)
+            return
         self._rollout(action_ring, n_steps, fused, storage, stats_out, drain)
         if check:
             torch.cuda.synchronize(self.device)
             self.check_health()
+
+    def _host_rollout(self, action_ring, n_steps, storage, stats_out, drain):
+        """The host build's rollout: ``n_steps`` VecTask.step calls (one C call without storage), every step's
+        outputs copied into ``storage`` rows when given, then the statistics.  Fused or not is the same here."""
+        H = L.host_lib()
+        n = self.num_envs
+        if action_ring is None:
+            ring, ring_len = (self._zero_actions[None] if self.uses_actions else None), 1
+        else:
+            if not isinstance(action_ring, torch.Tensor) or action_ring.dim() != 3 or \
+                    action_ring.shape[1:] != (n, self.num_actions):
+                raise ValueError("action_ring must be (T, num_envs, 4)")
+            ring = action_ring.to(device="cpu", dtype=torch.float32).contiguous()
+            ring_len = ring.shape[0]
+        if storage is None:
+            L.host_check(H.ouz_host_step_n(self._env, L.ptr(ring), ring_len, int(n_steps)), "ouz_host_step_n")
+        else:
+            obs, rew, rst, to = storage
+            for t, shape in ((obs, (n_steps, n, 13)), (rew, (n_steps, n)), (rst, (n_steps, n)), (to, (n_steps, n))):
+                if tuple(t.shape[:len(shape)]) != shape:
+                    raise ValueError(f"storage must be {shape}")
+            for k in range(int(n_steps)):
+                a = None if ring is None else ring[k % ring_len]
+                L.host_check(H.ouz_host_step(self._env, L.ptr(a) if a is not None else None), "ouz_host_step")
+                obs[k].copy_(self.obs_buf)
+                rew[k].copy_(self.rew_buf)
+                rst[k].copy_(self.reset_buf)
+                to[k].copy_(self.timeout_buf)
+        if stats_out is not None:
+            if stats_out.dtype != torch.float64 or stats_out.numel() < 3 or stats_out.device.type != "cpu":
+                raise ValueError("stats_out must be a float64 CPU tensor of >= 3")
+            L.host_check(H.ouz_host_episode_stats(self._env, L.ptr(stats_out), 1 if drain else 0),
+                         "ouz_host_episode_stats")
 
     def _rollout(self, action_ring, n_steps, fused, storage, stats_out, drain):
         if stats_out is not None:
@@ -475,6 +566,8 @@ class QuadVecTask:
         ``action_ring`` and ``storage`` alive while the plan is used.  The plan launches on torch's current
         stream of the env device at each call (not the one current when it was built), so it is ordered with
         the caller's work on that stream."""
+        if self._host:
+            raise NotImplementedError("rollout_plan pre-binds device pointers of the HIP path; use rollout()")
         if not self.cfg.track_episodes:
             raise RuntimeError("create the env with track_episodes=True")
         n_steps = int(n_steps)
@@ -516,7 +609,10 @@ class QuadVecTask:
     def reset_idx(self, env_ids):
         """Mark envs for the lazy reset applied at the start of the next step."""
         ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
-        L.check(L.lib.ouz_reset_idx(self._env, L.ptr(ids), ids.numel(), self._stream()), "ouz_reset_idx")
+        if self._host:
+            L.host_check(L.host_lib().ouz_host_reset_idx(self._env, L.ptr(ids), ids.numel()), "ouz_host_reset_idx")
+        else:
+            L.check(L.lib.ouz_reset_idx(self._env, L.ptr(ids), ids.numel(), self._stream()), "ouz_reset_idx")
         self._last_ids = ids
 
     def reset_done(self):
@@ -536,7 +632,7 @@ class QuadVecTask:
         """Env-state checkpoint (the reference never checkpoints env state).  The state is saved in
         slot order together with its layout marker; ``load_state_dict`` refuses a checkpoint of another layout.
         Raises (``check_health``) if a fused rollout since the last check gave up a split-wave wait."""
-        torch.cuda.synchronize(self.device)
+        self._sync()
         self.check_health()
         return {"fstate": self.fstate.clone(), "istate": self.istate.clone(), "obs": self.obs_buf.clone(),
                 "rew": self.rew_buf.clone(), "reset": self.reset_buf.clone(), "timeouts": self.timeout_buf.clone(),
@@ -567,7 +663,10 @@ class QuadVecTask:
         self.rew_buf.copy_(sd["rew"])
         self.reset_buf.copy_(sd["reset"])
         self.timeout_buf.copy_(sd["timeouts"])
-        L.check(L.lib.ouz_set_step(self._env, int(sd["step"])), "ouz_set_step")
+        if self._host:
+            L.host_check(L.host_lib().ouz_host_set_step(self._env, int(sd["step"])), "ouz_host_set_step")
+        else:
+            L.check(L.lib.ouz_set_step(self._env, int(sd["step"])), "ouz_set_step")
 
 
 def make(seed: int, task: str, num_envs: int, sim_device: str = "cuda:0", rl_device: str = "cuda:0",

@@ -1,5 +1,5 @@
-"""Helpers for the GPU parity tests: call the C ABI on torch tensors and map
-GPU SoA state <-> oracle (numpy) state.  Test infrastructure only."""
+"""Helpers for the parity tests: call the C ABI on torch tensors and map the env's SoA state (HIP device or
+the host build) <-> oracle (numpy) state.  Test infrastructure only."""
 import numpy as np
 import torch
 
@@ -42,7 +42,7 @@ def t(x, dtype=torch.float32):
 def gpu_to_oracle(env, oenv):
     """Copy a QuadVecTask's full state into an OracleEnv (float64)."""
     from ouzelum_amd import _lib as L
-    torch.cuda.synchronize()
+    env._sync()
     f = env.frows(0, L.F_COUNT).cpu().numpy().astype(np.float64)
     iv = env.irows(0, L.I_COUNT).cpu().numpy().astype(np.int64)
     oenv.p = f[L.F_P:L.F_P + 3].T.copy()
@@ -75,7 +75,7 @@ def gpu_to_oracle(env, oenv):
 
 def gpu_snapshot(env):
     from ouzelum_amd import _lib as L
-    torch.cuda.synchronize()
+    env._sync()
     f = env.frows(0, L.F_COUNT).cpu().numpy().astype(np.float64)
     iv = env.irows(0, L.I_COUNT).cpu().numpy()
     return {

@@ -35,6 +35,26 @@ def test_library_exports_every_header_symbol(L):
         assert hasattr(L.lib, n)
 
 
+def test_host_library_exports_every_host_header_symbol(L):
+    """libouzelum_cpu.so (make(sim_device="cpu")) exports exactly what include/ouzelum_host.h declares."""
+    src = open(os.path.join(ROOT, "include", "ouzelum_host.h")).read()
+    names = sorted(set(re.findall(r"\b(ouz_host_[a-z0-9_]+)\s*\(", src)))
+    assert len(names) >= 14
+    out = subprocess.run(["nm", "-D", "--defined-only", L.HOST_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (ouz_\w+)", out))
+    assert set(names) == exported, (set(names) ^ exported)
+    assert set(names) == set(L.HOST_SIGNATURES)
+    H = L.host_lib()
+    assert H.ouz_host_abi_version() == L.ABI_VERSION
+    cfg = L.OuzConfig()
+    L.lib.ouz_default_config(cfg)
+    cfg.task = 17
+    h = ctypes.c_void_p()
+    assert H.ouz_host_create(cfg, h) == -1 and b"unknown task" in H.ouz_host_last_error()
+    assert H.ouz_host_step(None, None) == -3
+
+
 def test_header_constants_match_python_mirror(L):
     src = open(HEADER).read()
     defines = dict(re.findall(r"#define (OUZ_\w+) \(?(-?\d+)\)?", src))
@@ -83,10 +103,19 @@ def test_task_info(L):
 
 
 def test_no_cpu_fallback():
+    """A HIP env never falls back to the CPU: without a visible device, sim_device="cuda:0" raises.  The host
+    build is reached only by asking for it (sim_device="cpu"), and reports itself as such."""
+    import torch
+
     import ouzelum_amd as o
     from ouzelum_amd._lib import OuzelumError
-    with pytest.raises(OuzelumError):
-        o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="cpu", rl_device="cpu")
+    if not torch.cuda.is_available():
+        with pytest.raises(OuzelumError):
+            o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="cuda:0", rl_device="cuda:0")
+    env = o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="cpu", rl_device="cpu")
+    assert env._host and env.fstate.device.type == "cpu"
+    with pytest.raises(ValueError):
+        o.make(seed=0, task="LeeLanded", num_envs=64, sim_device="meta")
 
 
 def test_state_slots_and_class_layout_map(L):
