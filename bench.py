@@ -122,13 +122,43 @@ def task_dtype(task):
 
 
 # ----------------------------------------------------------------------------------------- CPU baseline
+def host_build_rows(runs, seed, budget_s, cores):
+    """The build's own f32 CPU step (``make(sim_device="cpu")``: libouzelum_cpu.so, the HIP path's quad_env.h /
+    quad_math.h compiled for the host, OpenMP over envs on ``cores`` threads) for each BASELINE config: BASELINE.md
+    §4.2's vectorised f32 CPU restatement.  Each config runs 16-step rollouts for ``budget_s`` seconds after one
+    warm-up rollout.  Runs after the oracle's forked workers (no fork follows an OpenMP start)."""
+    import ouzelum_amd
+    rows = []
+    for letter, t, s, off, tot in runs:
+        env = ouzelum_amd.make(seed=seed, task=t, num_envs=s, sim_device="cpu", rl_device="cpu",
+                               env_id_offset=off, num_envs_total=tot, host_threads=cores)
+        ring = (torch.rand((RING, s, 4), generator=torch.Generator().manual_seed(seed)) * 2 - 1).contiguous()
+        env.rollout(ring, RING)
+        steps, t0 = 0, time.perf_counter()
+        while True:
+            env.rollout(ring, RING)
+            steps += RING
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                break
+        v = s * steps / el
+        rows.append({"config": letter, "task": t, "num_envs": s, "value": round(v, 1), "unit": "env-steps/s",
+                     "cores": cores, "steps": steps, "seconds": round(el, 3),
+                     "sample": f"f32 host build (libouzelum_cpu.so), {t}, {s} envs on {cores} OpenMP threads x "
+                               f"{steps} steps ({el:.2f} s)"})
+        print(f"cpu baseline (f32 host build): {t} {s} envs on {cores} threads: {v:.4g} env-steps/s", file=sys.stderr,
+              flush=True)
+        del env
+    return rows
+
+
 def cpu_baseline_leg(task, n, seed, budget_s):
     """The float64 numpy restatement of the step (oracle/quad_oracle.py, "port") in one process per host core
     of this box (oracle/cpu_bench.py), for every BASELINE config: A (Ouzelum, 64 envs), B and C at
     N = 64 / 4096 / 8192, D (QuadFault, 8192), E's per-GPU shard (QuadMixed, global ids 0-4095 of 32768),
-    plus the reference-structure per-env estimator loop, one thread.  BASELINE.md §4 names a torch-CPU f32
-    restatement; this build's CPU restatement is numpy f64 (the parity oracle), reported as such.  Runs before
-    the GPU is initialised (the worker processes are forked)."""
+    plus the reference-structure per-env estimator loop, one thread.  Beside it (``f32_host``), the build's own
+    f32 host step on the same cores for A-E (BASELINE.md §4.2's vectorised f32 CPU baseline).  Runs before the GPU
+    is initialised (the oracle's worker processes are forked)."""
     from oracle import cpu_bench as C
     cores = C.host_cores()
     sizes = [64, 4096, 8192]
@@ -137,7 +167,7 @@ def cpu_baseline_leg(task, n, seed, budget_s):
                                                                   ("E", "QuadMixed", 4096, 0, 32768)])
     if (task, n) not in {(t, s) for _, t, s, _, _ in runs}:
         runs.insert(0, (TASK_CONFIG.get(task, "-"), task, n, 0, n))
-    per = budget_s * 0.85 / len(runs)
+    per = budget_s * 0.7 / len(runs)
     table = []
     for letter, t, s, off, tot in runs:
         r = C.vectorised(t, s, seed=seed, budget_s=per, cores=cores, env_id_offset=off, n_total=tot)
@@ -146,13 +176,17 @@ def cpu_baseline_leg(task, n, seed, budget_s):
         print(f"cpu baseline: {t} {s} envs on {r['cores']} cores: {r['value']:.4g} env-steps/s", file=sys.stderr,
               flush=True)
     head = next(r for r in table if r["task"] == task and r["num_envs"] == n)
-    ref = C.reference_structure(n=16, budget_s=budget_s * 0.15)
+    ref = C.reference_structure(n=16, budget_s=budget_s * 0.1)
+    host_runs = [r for r in runs if r[0] in "ABCDE" and (r[0] not in "BC" or r[2] == 4096)]
+    if (task, n) not in {(t, s) for _, t, s, _, _ in host_runs}:
+        host_runs.insert(0, (TASK_CONFIG.get(task, "-"), task, n, 0, n))
+    f32 = host_build_rows(host_runs, seed, budget_s * 0.2 / len(host_runs), cores)
     return {"value": head["value"], "unit": "env-steps/s", "cores": head["cores"], "kind": "port",
             "sample": head["sample"] + f"; host {C.host_model()}, {cores} cores available (affinity / cgroup quota "
                                        "/ OMP_NUM_THREADS)",
-            "leg": "f64 numpy restatement of the step, one process per core (BASELINE.md §4 names a torch-CPU "
-                   "f32 restatement; this build's CPU restatement is the f64 parity oracle)",
-            "host_cores": cores, "host_model": C.host_model(), "table": table,
+            "leg": "f64 numpy restatement of the step (the parity oracle), one process per core; f32_host: the "
+                   "build's own f32 host step (BASELINE.md §4.2's vectorised f32 CPU restatement) on the same cores",
+            "host_cores": cores, "host_model": C.host_model(), "table": table, "f32_host": f32,
             "reference_structure_estimator": {**ref, "config": "C"}}
 
 

@@ -127,8 +127,9 @@ int host_steps(ouz_host_env* env, const float* ring, int32_t ring_len, int32_t n
     const StepCtx sc{step, flicker_mask(a, task, step),
                      ring ? ring + (size_t)(k % ring_len) * (size_t)a.n * OUZ_NUM_ACT : nullptr};
     if (a.trace_cap > 0) a.trace_resets[step % (uint32_t)a.trace_cap] = 0u;
-    // 64-slot chunks (one state tile) per scheduling unit: a thread walks whole tiles
-#pragma omp parallel for schedule(static) num_threads(nt) if (n_slots > 256)
+    // one state tile (64 slots) per scheduling unit, handed out dynamically: tiles differ in cost (the PV
+    // fixes of a trigger class, the curriculum's task per 1344-id chunk)
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt) if (n_slots > 256)
     for (int t = 0; t < (n_slots + 63) / 64; ++t) {
       const int hi = (t + 1) * 64 < n_slots ? (t + 1) * 64 : n_slots;
       for (int i = t * 64; i < hi; ++i) host_slot_step(a, sc, task, i);

@@ -170,8 +170,9 @@ class QuadVecTask:
     def __del__(self):
         env = getattr(self, "_env", None)
         if env is not None and env.value and getattr(self, "_host", False):
-            if L._hostlib is not None:
-                L._hostlib.ouz_host_destroy(env)
+            hl = getattr(L, "_hostlib", None) if L is not None else None   # None during interpreter shutdown
+            if hl is not None:
+                hl.ouz_host_destroy(env)
             self._env = None
             return
         if env is not None and env.value:
