@@ -260,6 +260,36 @@ def load_traffic(kernel, task, n):
     return {"bytes_per_launch": None, "stale": f"no summary of library {sha}; newest of another build: {newest_other}"}
 
 
+NOMINAL_CLOCK_GHZ = 2.4   # the in-kernel clock of an unloaded MI355X (s_memtime probes, profiles/r03/valu_issue.jsonl)
+
+
+def load_issue(kernel, task, n):
+    """The issue-bound view of this kernel at this size from a committed scripts/gpu_valu.sh summary of THIS
+    library build (PMC passes of SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* / SQ_INSTS_VALU and f64 counts), or
+    None.  For the kernels that are not HBM-bound: where their time goes instead.
+    ``kernel_us_from_counters``: one wave's lifetime at the nominal clock (latency regime: one wave per SIMD, the
+    launch lasts about one wave) or the PMC pass's kernel cycles at its own clock (large N)."""
+    import glob
+    mode = "rollout" if kernel == "rollout" else "step"
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", f"valu_*_{mode}_{task}_{n}_summary.json"),
+                            recursive=True))
+    sha = loaded_lib_sha16()
+    for h in reversed(hits):
+        with open(h) as fh:
+            d = json.load(fh)
+        if d.get("lib_sha16") != sha:
+            continue
+        lat = n <= LATENCY_REGIME_ENVS
+        us = d["wave_cycles"] / (NOMINAL_CLOCK_GHZ * 1e3) if lat else d["kernel_cycles"] / (d["clock_ghz"] * 1e3)
+        return {"bound": "valu-issue" if d["valu_active_frac"] >= 0.5 or lat else "mixed",
+                "valu_issue_frac": d["valu_issue_frac"], "valu_active_frac": d["valu_active_frac"],
+                "issue_active_frac": d["issue_active_frac"], "wait_frac": d["wait_frac"],
+                "chip_valu_frac": d["chip_valu_frac"], "simd_frac": d["simd_frac"], "f64_share": d["f64_share"],
+                "valu_insts_per_wave_step": d["valu_insts_per_wave_step"], "wave_cycles": d["wave_cycles"],
+                "kernel_us_from_counters": round(us, 3), "source": os.path.relpath(h, ROOT)}
+    return None
+
+
 def streamed_rollout(task, n):
     """ouz_rollout of the tasks without the estimator above 131 072 envs: one step launch per step into the
     storage rows (stream_rollout_default in quad_kernels.hip)."""
@@ -300,6 +330,9 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
          "steps_per_launch": 1 if streamed else steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
          "bytes_per_launch": round(b * n * (1 if streamed else steps_per_launch)), "kernel_us": round(us_per_step, 3),
          "kernel_us_per_launch": round(us_per_step * (1 if streamed else steps_per_launch), 3)}
+    issue = None if streamed else load_issue(kernel, task, n)
+    if issue:
+        e["issue"] = issue
     if streamed and traffic:
         # the summary's rocprof average is the step launches' alone; the rollout's per-rollout last-row copy and
         # statistics launch (in b, and in the HIP-event time) are not in it, so no rocprof-priced fraction here

@@ -6,7 +6,9 @@ Counter units (MI355X_MICROARCH.md §rocprofv3 / the counter descriptions of `ro
 SQ_WAVE_CYCLES, SQ_ACTIVE_INST_*, SQ_WAIT_* are wave quad-cycles summed over the waves; SQ_WAIT_ANY +
 SQ_WAIT_INST_ANY + SQ_ACTIVE_INST_ANY ~= SQ_WAVE_CYCLES; GRBM_GUI_ACTIVE is GPU-busy cycles summed over the 8
 XCDs.  Derived, per dispatch of the kernel (averaged over its dispatches):
-  clock_ghz          GRBM_GUI_ACTIVE / 8 / the dispatch's duration (kernel trace of the same pass)
+  clock_ghz          GRBM_GUI_ACTIVE / 8 / the dispatch's duration (kernel trace of the same pass; reads high on
+                     dispatches shorter than ~0.3 ms, the guide's DVFS note)
+  wave_cycles        one wave's lifetime in shader cycles, SQ_WAVE_CYCLES * 4 / SQ_WAVES; kernel_cycles GRBM / 8
   wave_us            one wave's lifetime, SQ_WAVE_CYCLES * 4 / SQ_WAVES / clock
   valu_active_frac   SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: share of a wave's life its VALU instructions occupy
   issue_active_frac  SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES (any instruction issuing); wait_frac (s_waitcnt /
@@ -77,6 +79,7 @@ def main():
     res = {"task": task, "num_envs": n, "mode": mode, "kernel": kname.rstrip("<"), "steps_per_launch": steps,
            "dispatches": [len(v1), len(v2)], "lib_sha16": lib_sha16(), "counters_pass1": c, "counters_pass2": c2,
            "kernel_us_pmc_pass": round(dur_us, 3), "clock_ghz": round(clock, 3),
+           "wave_cycles": round(wc * 4 / waves, 1), "kernel_cycles": round(kcyc, 1),
            "wave_us": round(wc * 4 / waves / (clock * 1e3), 3),
            "valu_active_frac": round(c["SQ_ACTIVE_INST_VALU"] / wc, 4),
            "issue_active_frac": round(c["SQ_ACTIVE_INST_ANY"] / wc, 4),
