@@ -799,6 +799,17 @@ __global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, Rol
   step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 
+#ifdef OUZ_WIDE_ROLLOUT_WPE
+// A/B build only (-DOUZ_WIDE_ROLLOUT_WPE=w): the estimator tasks' fused rollout above the latency regime with the
+// register budget of w waves per SIMD (the default instantiation holds 256 VGPRs + AGPR spills, one wave).
+template <int TASK>
+__global__ void __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(OUZ_WIDE_ROLLOUT_WPE, OUZ_WIDE_ROLLOUT_WPE)))
+quad_rollout_wide_kernel(StepArgs a, RolloutArgs r) {
+  prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
+  step_body<TASK, true, false, false, false, false, false, false>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+}
+#endif
+
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
 // smaller grid walks tiles t, t + stride, ...; before computing tile t it issues the state loads of tile
 // t + stride, so a wave keeps a load batch in flight while it computes instead of alternating load ->
@@ -1476,6 +1487,10 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false>), g, b, 0, s, a, r.ctx[0]);
   else if (T != OUZ_TASK_MIXED && a.outw)
     hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, T != OUZ_TASK_MIXED>), g, dim3(128), 0, s, a, r);
+#ifdef OUZ_WIDE_ROLLOUT_WPE
+  else if (class_layout_task(T) && a.n > kLatencyRegimeEnvs)
+    hipLaunchKernelGGL((quad_rollout_wide_kernel<T>), g, b, 0, s, a, r);
+#endif
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 
