@@ -556,25 +556,31 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Grid reduction of the lanes' episode statistics (see RolloutStats).  Called once by each of the nw live waves
-// (w = its index in 0..nw-1, the partials' fixed summation order).
+// (w = its index in 0..nw-1, the partials' fixed summation order).  The last wave to add to the ticket sums the
+// partials.  The hand-off is the write-through form of MI355X_MICROARCH.md "Valid forms" (first row): each wave's
+// lane 0 stores its partials sc1 (write-through past the XCD's L2), drains them, then makes its agent-scope add;
+// the last adder reads every partial with sc1 loads once its add has returned.  No __threadfence(): its L2
+// writeback + invalidate (≈3.5 µs, the guide's price list) sat at the end of every fused rollout launch (16-step
+// LeeLanded launch 26.8 -> 23.6 µs without the statistics: profiles/r04/stats_tail.jsonl).
 __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, uint32_t w, uint32_t nw, const LaneStats& ls) {
   const uint32_t lane = threadIdx.x & 63u;
   const double s = wave_sum(ls.sum), c = wave_sum(ls.cnt), l = wave_sum(ls.len);
   uint32_t last = 0;
   if (lane == 0u) {
-    rs.partials[w * 3u + 0u] = s;
-    rs.partials[w * 3u + 1u] = c;
-    rs.partials[w * 3u + 2u] = l;
-    __threadfence();
-    last = atomicAdd(rs.ticket, 1u) == nw - 1u ? 1u : 0u;
+    double* p = rs.partials + w * 3u;
+    __hip_atomic_store(p + 0, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 2, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(rs.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nw - 1u ? 1u : 0u;
   }
   last = __shfl(last, 0, 64);
   if (!last) return;
-  __threadfence();
   double t[3] = {0.0, 0.0, 0.0};
   for (uint32_t j = lane; j < nw; j += 64u) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) t[k] += __builtin_nontemporal_load(&rs.partials[j * 3u + (uint32_t)k]);
+    for (int k = 0; k < 3; ++k)
+      t[k] += __hip_atomic_load(&rs.partials[j * 3u + (uint32_t)k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) t[k] = wave_sum(t[k]);
@@ -582,7 +588,7 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, uint32_t w,
     rs.out[0] = t[0];
     rs.out[1] = t[1];
     rs.out[2] = t[2];
-    *rs.ticket = 0u;   // ready for the next launch
+    *rs.ticket = 0u;   // ready for the next launch (visible to it after this kernel's end-of-kernel release)
   }
 }
 
@@ -792,23 +798,21 @@ __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx
 }
 
 // ouz_rollout: K <= kMaxRolloutChunk steps in one launch, env state kept in registers.  SPW: the split-wave
-// estimator form (quad_pv_split.h), 128-thread blocks.
-template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false, bool OWV = false>
-__global__ void __launch_bounds__(kMaxBlock) quad_rollout_kernel(StepArgs a, RolloutArgs r) {
+// estimator form (quad_pv_split.h), 128-thread blocks.  WPE: waves per SIMD the register budget is cut for (1: no
+// constraint).  The estimator tasks above the latency regime use WPE = 2 (rollout_wpe): unconstrained, their
+// K-step state holds 256 VGPRs + ~80 AGPRs, one wave per SIMD, and the wave's dependent chain leaves the VALU
+// idle a third of the time; at two waves per SIMD the compiler spills ~90 VGPRs to scratch (L1/L2-resident) and
+// the rollout runs 10-12 % faster per step at 4 M envs (QuadTracking 410 -> 359 us, QuadMixed 380 -> 344:
+// profiles/r04/wide_rollout_ab.txt).
+template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false, bool OWV = false, int WPE = 1>
+__global__ void __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE)))
+quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
   step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
-
-#ifdef OUZ_WIDE_ROLLOUT_WPE
-// A/B build only (-DOUZ_WIDE_ROLLOUT_WPE=w): the estimator tasks' fused rollout above the latency regime with the
-// register budget of w waves per SIMD (the default instantiation holds 256 VGPRs + AGPR spills, one wave).
-template <int TASK>
-__global__ void __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(OUZ_WIDE_ROLLOUT_WPE, OUZ_WIDE_ROLLOUT_WPE)))
-quad_rollout_wide_kernel(StepArgs a, RolloutArgs r) {
-  prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true, false, false, false, false, false, false>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+__host__ __device__ constexpr int rollout_wpe(int task, int n) {
+  return class_layout_task(task) && n > kLatencyRegimeEnvs ? 2 : 1;
 }
-#endif
 
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
 // smaller grid walks tiles t, t + stride, ...; before computing tile t it issues the state loads of tile
@@ -1487,10 +1491,8 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false>), g, b, 0, s, a, r.ctx[0]);
   else if (T != OUZ_TASK_MIXED && a.outw)
     hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, T != OUZ_TASK_MIXED>), g, dim3(128), 0, s, a, r);
-#ifdef OUZ_WIDE_ROLLOUT_WPE
-  else if (class_layout_task(T) && a.n > kLatencyRegimeEnvs)
-    hipLaunchKernelGGL((quad_rollout_wide_kernel<T>), g, b, 0, s, a, r);
-#endif
+  else if (class_layout_task(T) && rollout_wpe(T, a.n) == 2)
+    hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, false, (class_layout_task(T) ? 2 : 1)>), g, b, 0, s, a, r);
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 
