@@ -764,9 +764,10 @@ def main():
         "config": {"workload": f"config {letter}: {n}-env {desc} ({args.task}), dt 0.01 x 2 sub-steps; "
                                f"16-step rollouts, one persistent launch each (ouz_rollout_stats)",
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
-                   "parallelism": f"env-sharded dp{world} (per-16-step-rollout return statistics, async "
-                                  f"{'RCCL' if backend == 'nccl' else backend or 'no'} all-reduce of "
-                                  f"{args.allreduce_batch} rollouts' rows per collective)",
+                   "parallelism": (f"env-sharded dp{world} (per-16-step-rollout return statistics, async "
+                                   f"{'RCCL' if backend == 'nccl' else backend} all-reduce of "
+                                   f"{args.allreduce_batch} rollouts' rows per collective)") if world > 1 else
+                                  "dp1 (one GPU; each rollout's return statistics reduced inside its launch)",
                    "ranks_joined": world, "physical_devices": min(world, n_dev), "backend": backend,
                    "collective": red.collective if world > 1 else None, "rccl_comm_count": comm_count,
                    "launcher": "bench.py" if os.environ.get("OUZ_BENCH_SPAWNED") else (

@@ -810,8 +810,11 @@ quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
   step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
+#ifndef OUZ_EST_ROLLOUT_WPE
+#define OUZ_EST_ROLLOUT_WPE 2   // (A/B builds: -DOUZ_EST_ROLLOUT_WPE=3)
+#endif
 __host__ __device__ constexpr int rollout_wpe(int task, int n) {
-  return class_layout_task(task) && n > kLatencyRegimeEnvs ? 2 : 1;
+  return class_layout_task(task) && n > kLatencyRegimeEnvs ? OUZ_EST_ROLLOUT_WPE : 1;
 }
 
 // Large-N VecTask.step with the next tile's state in flight during this tile's compute.  Each wave of a
@@ -1491,8 +1494,9 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false>), g, b, 0, s, a, r.ctx[0]);
   else if (T != OUZ_TASK_MIXED && a.outw)
     hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, T != OUZ_TASK_MIXED>), g, dim3(128), 0, s, a, r);
-  else if (class_layout_task(T) && rollout_wpe(T, a.n) == 2)
-    hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, false, (class_layout_task(T) ? 2 : 1)>), g, b, 0, s, a, r);
+  else if (class_layout_task(T) && rollout_wpe(T, a.n) > 1)
+    hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, false, (class_layout_task(T) ? OUZ_EST_ROLLOUT_WPE : 1)>), g, b,
+                       0, s, a, r);
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 
