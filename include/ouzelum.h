@@ -228,6 +228,10 @@ typedef struct ouz_task_info {
 typedef struct ouz_env ouz_env;
 
 int32_t ouz_abi_version(void);
+/* 16 hex digits identifying the sources and flags this library was built from (ouzelum_amd/build.py source_id):
+ * two builds of the same sources differ in bytes (hipcc's per-build unit ids), so profiling evidence is tied to
+ * a library by this id. */
+const char* ouz_source_id(void);
 /* Instrumentation compiled into this library (0 for the product build): timing-stamp builds and
  * store-policy A/B builds give the product's results but are not the product; the Python shim
  * refuses them unless OUZ_ALLOW_INSTRUMENTED=1 (tests/test_abi.py checks the shipped library is 0). */

@@ -88,6 +88,7 @@ _I64 = ctypes.c_int64
 # name -> (restype, argtypes).  This table IS the list of symbols include/ouzelum.h declares.
 SIGNATURES = {
     "ouz_abi_version": (_I, []),
+    "ouz_source_id": (ctypes.c_char_p, []),
     "ouz_build_flags": (_U32, []),
     "ouz_split_timeouts": (_I, [_P, _I]),
     "ouz_set_split_spin_limit": (_I, [_U32]),

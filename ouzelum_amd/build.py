@@ -62,6 +62,19 @@ def up_to_date(out=OUT, deps=DEPS) -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
+def source_id(extra=()) -> str:
+    """16 hex digits of sha256 over the library's sources (DEPS, in order) and its build flags.  Compiled into the
+    library (``ouz_source_id()``): hipcc names every compilation unit with a random id that ends up in the
+    binary, so two builds of the same sources differ in bytes; PMC evidence is matched to a library by this id."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in DEPS:
+        with open(d, "rb") as fh:
+            h.update(os.path.relpath(d, ROOT).encode() + b"\0" + fh.read() + b"\0")
+    h.update(" ".join([*FLAGS, *extra]).encode())
+    return h.hexdigest()[:16]
+
+
 def build_host(force: bool = False, verbose: bool = True) -> str:
     """libouzelum_cpu.so: quad_host.cpp (quad_env.h + quad_math.h for the host) with g++ and OpenMP."""
     if not force and up_to_date(HOST_OUT, HOST_DEPS):
@@ -79,7 +92,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return OUT
     extra = os.environ.get("OUZ_EXTRA_FLAGS", "").split()
-    cmd = [HIPCC, *FLAGS, *extra, "-o", OUT + ".tmp", *SRCS]
+    sid = source_id(extra)
+    cmd = [HIPCC, *FLAGS, *extra, f'-DOUZ_SOURCE_ID="{sid}"', "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -1293,6 +1293,11 @@ int ouz_probe_stamps(uint64_t* host, int32_t count) {
 
 int32_t ouz_abi_version(void) { return OUZ_ABI_VERSION; }
 
+#ifndef OUZ_SOURCE_ID
+#define OUZ_SOURCE_ID "unknown"
+#endif
+const char* ouz_source_id(void) { return OUZ_SOURCE_ID; }
+
 uint32_t ouz_build_flags(void) {
   uint32_t f = 0;
 #ifdef OUZ_STAMPS

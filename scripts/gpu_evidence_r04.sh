@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-4 evidence of ONE library build, in two gpurun calls (each under the 20-minute limit):
+#   bash scripts/gpu_evidence_r04.sh TAG a   GPU suite, smoke(), roofline evidence (rocprofv3 --stats + FETCH_SIZE /
+#                                            WRITE_SIZE passes) of the headline-size entries, VALU / issue passes
+#                                            of every entry that is not HBM-bound
+#   bash scripts/gpu_evidence_r04.sh TAG b   roofline evidence of the large-N sweep, then the bench lines (driver
+#                                            arguments, no flags) and rocprofv3 --stats of the driver's command
+# Summaries land in gpurun_out/ (copied into profiles/r04/ by hand between the calls; part b stages its own into
+# profiles/r04/roofline on the box so that its bench lines price traffic from them).  Stops at the first failure.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+TAG=$1; PART=$2
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+step() { local name=$1; shift; local lim=$1; shift
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -n 20 "$OUT/$name.out" "$OUT/$name.err"; exit $rc; }; }
+if [ "$PART" = a ]; then
+  step pytest 600 python -u -m pytest tests -m gpu -q -x --timeout 180 --timeout-method thread -p no:cacheprovider
+  tail -n 2 "$OUT/pytest.out"
+  step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
+  bash scripts/gpu_roofline_evidence.sh "$TAG" \
+    rollout:LeeLanded:4096 step:LeeLanded:4096 rollout:QuadTracking:4096 step:QuadTracking:4096 \
+    rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 > "$OUT/evidence_headline.log" 2>&1 \
+    || { tail -n 20 "$OUT/evidence_headline.log"; exit 1; }
+  echo "evidence headline ok"
+  bash scripts/gpu_valu.sh "$TAG" rollout:LeeLanded:4096 step:LeeLanded:4096 rollout:QuadTracking:4096 \
+    step:QuadTracking:4096 rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 \
+    rollout:QuadTracking:4194304 rollout:QuadMixed:4194304 rollout:QuadTracking:16777216 rollout:QuadMixed:16777216 \
+    > "$OUT/valu.log" 2>&1 || { tail -n 20 "$OUT/valu.log"; exit 1; }
+  echo "valu ok"
+else
+  bash scripts/gpu_roofline_evidence.sh "$TAG" > "$OUT/evidence_large.log" 2>&1 || { tail -n 20 "$OUT/evidence_large.log"; exit 1; }
+  echo "evidence large-N ok"
+  mkdir -p profiles/r04/roofline
+  for f in gpurun_out/pmc_${TAG}_*_summary.json; do
+    b=$(basename "$f" _summary.json)
+    cp "$f" profiles/r04/roofline/ && cp "gpurun_out/${b}_STATS/run_kernel_stats.csv" "profiles/r04/roofline/${b}_kernel_stats.csv"
+  done
+  step bench_driver 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/bench_detail_driver.json"
+  step bench_default 500 python -u bench.py --detail "$OUT/bench_detail_default.json"
+  export TMPDIR=/tmp
+  step prof_driver 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/$OUT/prof" -o run -- \
+    python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-sweep --no-configs --detail "$OUT/bench_detail_prof.json"
+  tail -c 300 "$OUT/bench_driver.out"; echo
+  tail -c 300 "$OUT/bench_default.out"; echo
+fi

@@ -22,7 +22,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def lib_sha16(path=None):
+    """The library's source id (ouz_source_id(): its sources and build flags, stable across rebuilds), or for a
+    library without one, the sha256 of its bytes.  PMC / VALU summaries carry it; bench.py prices evidence only
+    from summaries of the library it loaded."""
+    import ctypes
     path = path or os.environ.get("OUZ_LIB") or os.path.join(ROOT, "ouzelum_amd", "libouzelum_hip.so")
+    try:
+        lib = ctypes.CDLL(path)
+        fn = lib.ouz_source_id
+        fn.restype = ctypes.c_char_p
+        sid = fn().decode()
+        if sid and sid != "unknown":
+            return "src-" + sid
+    except (OSError, AttributeError):
+        pass
     with open(path, "rb") as fh:
         return hashlib.sha256(fh.read()).hexdigest()[:16]
 

@@ -35,6 +35,14 @@ def test_library_exports_every_header_symbol(L):
         assert hasattr(L.lib, n)
 
 
+def test_library_built_from_these_sources(L):
+    """ouz_source_id() of the in-tree library = the id of the sources and flags in this tree (build.source_id):
+    the .so the tests and the bench load is the build of this checkout, and PMC evidence matched by that id
+    (bench.py load_traffic) belongs to it."""
+    from ouzelum_amd import build as b
+    assert L.lib.ouz_source_id().decode() == b.source_id()
+
+
 def test_host_library_exports_every_host_header_symbol(L):
     """libouzelum_cpu.so (make(sim_device="cpu")) exports exactly what include/ouzelum_host.h declares."""
     src = open(os.path.join(ROOT, "include", "ouzelum_host.h")).read()
