@@ -51,6 +51,32 @@ def test_direct_collectives_on_rccl():
     assert res == {"ranges": 2 * 4 * 5 // 2, "unchanged": True}
 
 
+@pytest.mark.parametrize("form", ["eager", "direct"])
+def test_rccl_two_ranks_both_collective_forms(form):
+    """ReturnAllReduce over a real two-rank RCCL group (one GPU per rank), in both collective forms: every rank
+    agrees on the form (the direct one falls back to eager on all ranks together if its check fails), the rows
+    reduce to their closed-form sums, and the communicator reports two ranks.  Needs two devices: skipped on the
+    one-GPU box, run wherever two or more MI355X are visible (the direct form had only run at one rank)."""
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs two HIP devices")
+    import json
+    world, port = 2, _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), LOCAL_RANK=str(r),
+                   WORLD_SIZE=str(world), OUZ_COLLECTIVE=form,
+                   PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_rccl_ranks_worker.py")],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=180) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, (o + e)[-3000:]
+    res = json.loads(outs[0][0].strip().splitlines()[-1])
+    assert len(res) == world and all(r["ok"] for r in res), res
+    assert len({r["collective"] for r in res}) == 1
+    assert all(r["comm_count"] in (None, world) for r in res)
+
+
 @pytest.mark.parametrize("task,n,rollouts", [("QuadMixed", 4096, 12), ("QuadFault", 1000, 10)])
 def test_two_rank_hip_shards_match_single_process(tmp_path, task, n, rollouts):
     if not torch.cuda.is_available():
