@@ -603,18 +603,27 @@ def spawn_ranks(args):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
     rc = 0
     live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 128 - code
-                print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
-                for q in live:   # the exact children started above, never a pattern
-                    q.send_signal(signal.SIGTERM)
-        time.sleep(0.05)
+
+    def stop(sig, _frame=None):   # a signal to the parent (e.g. a time limit) reaches the ranks it started
+        for q in live:
+            q.send_signal(sig)
+    old = {s: signal.signal(s, stop) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench: rank {procs.index(p)} exited with {code}; stopping the other ranks", file=sys.stderr)
+                    for q in live:   # the exact children started above, never a pattern
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.05)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
     return rc
 
 
