@@ -1,0 +1,81 @@
+"""Where the wall time of bench.py's timed region goes at N = 1 (config B, 16 + 4 steps): host checkpoints with
+perf_counter inside the same sequence Runner.timed runs (start event, the two rollout launches, the end event,
+torch.cuda.synchronize), 300 repetitions, medians.  Variants of the wait at the end:
+  sync      torch.cuda.synchronize() alone (bench.py)
+  query     spin on hipEventQuery(end event) until it completes, then torch.cuda.synchronize()
+  evsync    hipEventSynchronize(end event), then torch.cuda.synchronize()
+Prints one JSON line per variant.
+
+    python scripts/exp/region_breakdown.py [task] [num_envs]
+"""
+import ctypes
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from ouzelum_amd.distributed import ReturnAllReduce  # noqa: E402
+
+
+def main():
+    task = sys.argv[1] if len(sys.argv) > 1 else "LeeLanded"
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    red = ReturnAllReduce(dev, batch=1)
+    run = bench.Runner(task, n, dev, 1, 0, 1, red)
+    run.rollouts(5)
+    run.prepare(20)
+    ev = bench.HipEvents(dev)
+    hip = ev.hip
+    ev.record(0)
+    ev.record(1)
+    torch.cuda.synchronize(dev)
+    reps = 300
+    for variant in ("sync", "query", "evsync", "sync", "query", "evsync"):
+        marks = []
+        gpu = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            time.sleep(0.0002)
+            pc = time.perf_counter
+            t0 = pc()
+            ev.record(0)
+            t1 = pc()
+            run.plan(16)(red.slot_ptr(run.n_roll))
+            t2 = pc()
+            run.plan(4)(red.slot_ptr(run.n_roll + 1))
+            t3 = pc()
+            run.n_roll += 2
+            red.finish()
+            ev.record(1)
+            t4 = pc()
+            if variant == "query":
+                while hip.hipEventQuery(ev.ev[1]) != 0:
+                    pass
+            elif variant == "evsync":
+                hip.hipEventSynchronize(ev.ev[1])
+            t5 = pc()
+            torch.cuda.synchronize(dev)
+            t6 = pc()
+            marks.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5, t6 - t0))
+            gpu.append(ev.elapsed_ms() * 1e3)
+        med = [statistics.median(m[i] for m in marks) * 1e6 for i in range(7)]
+        print(json.dumps({"variant": variant, "task": task, "num_envs": n, "reps": reps,
+                          "us": {"record_start": round(med[0], 2), "launch_16": round(med[1], 2),
+                                 "launch_4": round(med[2], 2), "finish_record_end": round(med[3], 2),
+                                 "wait": round(med[4], 2), "synchronize": round(med[5], 2),
+                                 "region": round(med[6], 2)},
+                          "gpu_us_median": round(statistics.median(gpu), 2),
+                          "region_us_min": round(min(m[6] for m in marks) * 1e6, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
