@@ -1,5 +1,8 @@
 #!/bin/bash
-# Round-4 evidence of ONE library build, in two gpurun calls (each under the 20-minute limit):
+# Round-4 evidence of ONE library build, in gpurun calls each under the 20-minute limit:
+#   bash scripts/gpu_evidence_r04.sh TAG h   the headline alone (when boxes are scarce): roofline + VALU evidence of
+#                                            config B's two kernels, staged, then smoke(), the driver-argument bench
+#                                            line and rocprofv3 --stats of the driver's command
 #   bash scripts/gpu_evidence_r04.sh TAG a   GPU suite, smoke(), roofline evidence (rocprofv3 --stats + FETCH_SIZE /
 #                                            WRITE_SIZE passes) of the headline-size entries, VALU / issue passes
 #                                            of every entry that is not HBM-bound
@@ -16,7 +19,31 @@ mkdir -p "$OUT"
 step() { local name=$1; shift; local lim=$1; shift
   timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
   local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -n 20 "$OUT/$name.out" "$OUT/$name.err"; exit $rc; }; }
-if [ "$PART" = a ]; then
+stage() {   # summaries of this build into profiles/r04 on the box, so that its bench lines price from them
+  mkdir -p profiles/r04/roofline profiles/r04/valu
+  for f in gpurun_out/pmc_${TAG}_*_summary.json; do
+    [ -e "$f" ] || continue
+    b=$(basename "$f" _summary.json)
+    cp "$f" profiles/r04/roofline/ && cp "gpurun_out/${b}_STATS/run_kernel_stats.csv" "profiles/r04/roofline/${b}_kernel_stats.csv"
+  done
+  for f in gpurun_out/valu_${TAG}_*_summary.json; do [ -e "$f" ] && cp "$f" profiles/r04/valu/; done
+  return 0; }
+driver_bench() {
+  step bench_driver 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/bench_detail_driver.json"
+  export TMPDIR=/tmp
+  step prof_driver 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/$OUT/prof" -o run -- \
+    python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-sweep --no-configs --detail "$OUT/bench_detail_prof.json"
+  tail -c 300 "$OUT/bench_driver.out"; echo; }
+if [ "$PART" = h ]; then
+  bash scripts/gpu_roofline_evidence.sh "$TAG" rollout:LeeLanded:4096 step:LeeLanded:4096 > "$OUT/evidence_h.log" 2>&1 \
+    || { tail -n 20 "$OUT/evidence_h.log"; exit 1; }
+  bash scripts/gpu_valu.sh "$TAG" rollout:LeeLanded:4096 step:LeeLanded:4096 > "$OUT/valu_h.log" 2>&1 \
+    || { tail -n 20 "$OUT/valu_h.log"; exit 1; }
+  echo "headline evidence ok"
+  stage
+  step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
+  driver_bench
+elif [ "$PART" = a ]; then
   step pytest 600 python -u -m pytest tests -m gpu -q -x --timeout 180 --timeout-method thread -p no:cacheprovider
   tail -n 2 "$OUT/pytest.out"
   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
@@ -33,16 +60,8 @@ if [ "$PART" = a ]; then
 else
   bash scripts/gpu_roofline_evidence.sh "$TAG" > "$OUT/evidence_large.log" 2>&1 || { tail -n 20 "$OUT/evidence_large.log"; exit 1; }
   echo "evidence large-N ok"
-  mkdir -p profiles/r04/roofline
-  for f in gpurun_out/pmc_${TAG}_*_summary.json; do
-    b=$(basename "$f" _summary.json)
-    cp "$f" profiles/r04/roofline/ && cp "gpurun_out/${b}_STATS/run_kernel_stats.csv" "profiles/r04/roofline/${b}_kernel_stats.csv"
-  done
-  step bench_driver 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 --detail "$OUT/bench_detail_driver.json"
+  stage
   step bench_default 500 python -u bench.py --detail "$OUT/bench_detail_default.json"
-  export TMPDIR=/tmp
-  step prof_driver 400 rocprofv3 --kernel-trace --stats -f csv -d "$R/$OUT/prof" -o run -- \
-    python3 -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-sweep --no-configs --detail "$OUT/bench_detail_prof.json"
-  tail -c 300 "$OUT/bench_driver.out"; echo
+  driver_bench
   tail -c 300 "$OUT/bench_default.out"; echo
 fi
