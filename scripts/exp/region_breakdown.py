@@ -4,9 +4,11 @@ torch.cuda.synchronize), 300 repetitions, medians.  Variants of the wait at the 
   sync      torch.cuda.synchronize() alone (bench.py)
   query     spin on hipEventQuery(end event) until it completes, then torch.cuda.synchronize()
   evsync    hipEventSynchronize(end event), then torch.cuda.synchronize()
+  empty     the region around one tiny torch kernel instead of the rollouts (the fixed floor)
 Prints one JSON line per variant.
 
-    python scripts/exp/region_breakdown.py [task] [num_envs]
+    python scripts/exp/region_breakdown.py [task] [num_envs] [variants, comma-separated]
+The HIP runtime's environment knobs in effect (ROC_* / HIP_FORCE_DEV_KERNARG) are printed with each line.
 """
 import ctypes
 import json
@@ -39,7 +41,10 @@ def main():
     ev.record(1)
     torch.cuda.synchronize(dev)
     reps = 300
-    for variant in ("sync", "query", "evsync", "sync", "query", "evsync"):
+    tiny = torch.zeros(64, device=dev)
+    variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["sync", "query", "evsync"] * 2
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("ROC_") or k == "HIP_FORCE_DEV_KERNARG"}
+    for variant in variants:
         marks = []
         gpu = []
         for _ in range(reps):
@@ -49,10 +54,14 @@ def main():
             t0 = pc()
             ev.record(0)
             t1 = pc()
-            run.plan(16)(red.slot_ptr(run.n_roll))
-            t2 = pc()
-            run.plan(4)(red.slot_ptr(run.n_roll + 1))
-            t3 = pc()
+            if variant == "empty":   # the floor: one tiny torch kernel in place of the two rollout launches
+                tiny.add_(1.0)
+                t2 = t3 = pc()
+            else:
+                run.plan(16)(red.slot_ptr(run.n_roll))
+                t2 = pc()
+                run.plan(4)(red.slot_ptr(run.n_roll + 1))
+                t3 = pc()
             run.n_roll += 2
             red.finish()
             ev.record(1)
@@ -74,7 +83,7 @@ def main():
                                  "wait": round(med[4], 2), "synchronize": round(med[5], 2),
                                  "region": round(med[6], 2)},
                           "gpu_us_median": round(statistics.median(gpu), 2),
-                          "region_us_min": round(min(m[6] for m in marks) * 1e6, 2)}), flush=True)
+                          "region_us_min": round(min(m[6] for m in marks) * 1e6, 2), "env": knobs}), flush=True)
 
 
 if __name__ == "__main__":
