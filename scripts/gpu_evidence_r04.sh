@@ -3,7 +3,7 @@
 #   bash scripts/gpu_evidence_r04.sh TAG h   the headline alone (when boxes are scarce): roofline + VALU evidence of
 #                                            config B's two kernels, staged, then smoke(), the driver-argument bench
 #                                            line and rocprofv3 --stats of the driver's command
-#   bash scripts/gpu_evidence_r04.sh TAG a   GPU suite, smoke(), roofline evidence (rocprofv3 --stats + FETCH_SIZE /
+#   bash scripts/gpu_evidence_r04.sh TAG a   (after h) GPU suite, smoke(), roofline evidence (rocprofv3 --stats + FETCH_SIZE /
 #                                            WRITE_SIZE passes) of the headline-size entries, VALU / issue passes
 #                                            of every entry that is not HBM-bound
 #   bash scripts/gpu_evidence_r04.sh TAG b   roofline evidence of the large-N sweep, then the bench lines (driver
@@ -48,12 +48,10 @@ elif [ "$PART" = a ]; then
   tail -n 2 "$OUT/pytest.out"
   step smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()"
   bash scripts/gpu_roofline_evidence.sh "$TAG" \
-    rollout:LeeLanded:4096 step:LeeLanded:4096 rollout:QuadTracking:4096 step:QuadTracking:4096 \
-    rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 > "$OUT/evidence_headline.log" 2>&1 \
+    rollout:QuadTracking:4096 step:QuadTracking:4096 rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 > "$OUT/evidence_headline.log" 2>&1 \
     || { tail -n 20 "$OUT/evidence_headline.log"; exit 1; }
   echo "evidence headline ok"
-  bash scripts/gpu_valu.sh "$TAG" rollout:LeeLanded:4096 step:LeeLanded:4096 rollout:QuadTracking:4096 \
-    step:QuadTracking:4096 rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 \
+  bash scripts/gpu_valu.sh "$TAG" rollout:QuadTracking:4096 step:QuadTracking:4096 rollout:QuadFault:8192 step:QuadFault:8192 rollout:QuadMixed:4096 step:QuadMixed:4096 \
     rollout:QuadTracking:4194304 rollout:QuadMixed:4194304 rollout:QuadTracking:16777216 rollout:QuadMixed:16777216 \
     > "$OUT/valu.log" 2>&1 || { tail -n 20 "$OUT/valu.log"; exit 1; }
   echo "valu ok"
