@@ -55,17 +55,20 @@ def roofline_table(d):
 
 def issue_table(d):
     rows = ["| workload | kernel | envs | µs/step | VALU issue frac | VALU active frac | issue active frac | "
-            "wait frac | SIMD frac | chip VALU frac | f64 share | µs from counters / launch | µs (HIP events) / launch |",
-            "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+            "wait frac | SIMD frac | chip VALU frac | f64 share | µs from counters / launch | rocprof avg µs / launch | "
+            "counters / rocprof |",
+            "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     for label, e in entries(d):
         iss = e.get("issue")
         if not iss:
             continue
         kern = e["kernel"].replace("quad_", "").replace("_kernel", "")
+        rp = (e.get("traffic_detail") or {}).get("rocprof_kernel_us_per_launch")
+        ratio = iss["kernel_us_from_counters"] / rp if rp else None
         rows.append(f"| {label} | {kern} | {e['num_envs']} | {fmt(e['kernel_us'])} | {fmt(iss['valu_issue_frac'])} | "
                     f"{fmt(iss['valu_active_frac'])} | {fmt(iss['issue_active_frac'])} | {fmt(iss['wait_frac'])} | "
                     f"{fmt(iss['simd_frac'])} | {fmt(iss['chip_valu_frac'])} | {fmt(iss['f64_share'])} | "
-                    f"{fmt(iss['kernel_us_from_counters'], 1)} | {fmt(e['kernel_us_per_launch'], 1)} |")
+                    f"{fmt(iss['kernel_us_from_counters'], 1)} | {fmt(rp, 1)} | {fmt(ratio, 2)} |")
     return "\n".join(rows)
 
 
