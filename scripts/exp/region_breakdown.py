@@ -5,6 +5,9 @@ torch.cuda.synchronize), 300 repetitions, medians.  Variants of the wait at the 
   query     spin on hipEventQuery(end event) until it completes, then torch.cuda.synchronize()
   evsync    hipEventSynchronize(end event), then torch.cuda.synchronize()
   empty     the region around one tiny torch kernel instead of the rollouts (the fixed floor)
+  noev      sync, without the two timing events (their own cost)
+Event flags (4th argument, an int): hipEventCreateWithFlags flags of the two timing events, e.g. 0x20000000
+(hipEventDisableSystemFence) or 0x40000000 (hipEventReleaseToDevice); default: hipEventCreate.
 Prints one JSON line per variant.
 
     python scripts/exp/region_breakdown.py [task] [num_envs] [variants, comma-separated]
@@ -37,6 +40,14 @@ def main():
     run.prepare(20)
     ev = bench.HipEvents(dev)
     hip = ev.hip
+    ev_flags = int(sys.argv[4], 0) if len(sys.argv) > 4 else None
+    if ev_flags is not None:   # replace the two events by ones created with these flags
+        for e in ev.ev:
+            hip.hipEventDestroy(e)
+        ev.ev = [ctypes.c_void_p(), ctypes.c_void_p()]
+        for e in ev.ev:
+            if hip.hipEventCreateWithFlags(ctypes.byref(e), ctypes.c_uint(ev_flags)) != 0:
+                raise RuntimeError("hipEventCreateWithFlags failed")
     ev.record(0)
     ev.record(1)
     torch.cuda.synchronize(dev)
@@ -52,7 +63,8 @@ def main():
             time.sleep(0.0002)
             pc = time.perf_counter
             t0 = pc()
-            ev.record(0)
+            if variant != "noev":
+                ev.record(0)
             t1 = pc()
             if variant == "empty":   # the floor: one tiny torch kernel in place of the two rollout launches
                 tiny.add_(1.0)
@@ -64,7 +76,8 @@ def main():
                 t3 = pc()
             run.n_roll += 2
             red.finish()
-            ev.record(1)
+            if variant != "noev":
+                ev.record(1)
             t4 = pc()
             if variant == "query":
                 while hip.hipEventQuery(ev.ev[1]) != 0:
@@ -75,7 +88,7 @@ def main():
             torch.cuda.synchronize(dev)
             t6 = pc()
             marks.append((t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4, t6 - t5, t6 - t0))
-            gpu.append(ev.elapsed_ms() * 1e3)
+            gpu.append(ev.elapsed_ms() * 1e3 if variant != "noev" else 0.0)
         med = [statistics.median(m[i] for m in marks) * 1e6 for i in range(7)]
         print(json.dumps({"variant": variant, "task": task, "num_envs": n, "reps": reps,
                           "us": {"record_start": round(med[0], 2), "launch_16": round(med[1], 2),
@@ -83,7 +96,8 @@ def main():
                                  "wait": round(med[4], 2), "synchronize": round(med[5], 2),
                                  "region": round(med[6], 2)},
                           "gpu_us_median": round(statistics.median(gpu), 2),
-                          "region_us_min": round(min(m[6] for m in marks) * 1e6, 2), "env": knobs}), flush=True)
+                          "region_us_min": round(min(m[6] for m in marks) * 1e6, 2), "env": knobs,
+                          "event_flags": ev_flags}), flush=True)
 
 
 if __name__ == "__main__":
