@@ -281,7 +281,9 @@ def load_issue(kernel, task, n):
             continue
         lat = n <= LATENCY_REGIME_ENVS
         us = d["wave_cycles"] / (NOMINAL_CLOCK_GHZ * 1e3) if lat else d["kernel_cycles"] / (d["clock_ghz"] * 1e3)
-        return {"bound": "valu-issue" if d["valu_active_frac"] >= 0.5 or lat else "mixed",
+        # latency regime: one wave per SIMD, bound by that wave's instruction chain ("valu-issue"); large N: by
+        # the chip's VALU throughput when its VALU pipes are busy at least half the kernel ("valu")
+        return {"bound": "valu-issue" if lat else ("valu" if d["chip_valu_frac"] >= 0.5 else "mixed"),
                 "valu_issue_frac": d["valu_issue_frac"], "valu_active_frac": d["valu_active_frac"],
                 "issue_active_frac": d["issue_active_frac"], "wait_frac": d["wait_frac"],
                 "chip_valu_frac": d["chip_valu_frac"], "simd_frac": d["simd_frac"], "f64_share": d["f64_share"],
@@ -333,6 +335,8 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
     issue = None if streamed else load_issue(kernel, task, n)
     if issue:
         e["issue"] = issue
+        if e["frac"] < 0.4:   # not HBM-bound: what binds it instead, from the counters
+            e["binding"] = issue["bound"]
     if streamed and traffic:
         # the summary's rocprof average is the step launches' alone; the rollout's per-rollout last-row copy and
         # statistics launch (in b, and in the HIP-event time) are not in it, so no rocprof-priced fraction here
@@ -629,7 +633,7 @@ def spawn_ranks(args):
 
 # ----------------------------------------------------------------------------------------- output
 LINE_LIMIT = 6000   # the stdout line stays well under what the driver parses (BENCH_r03's 26 KB line was not)
-_ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "frac_from_rocprof_avg", "kernel",
+_ROOF_KEYS = ("bound", "binding", "achieved", "peak", "unit", "frac", "traffic", "frac_from_rocprof_avg", "kernel",
               "steps_per_launch", "num_envs", "bytes_per_env_step", "kernel_us", "kernel_us_back_to_back")
 
 

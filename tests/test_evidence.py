@@ -56,3 +56,14 @@ def test_committed_bench_line_is_of_this_build():
     assert d["roofline"]["traffic"] and d["roofline"]["issue"]
     assert d["split_timeouts"] == 0
     assert len(json.dumps(d)) < B.LINE_LIMIT
+
+
+def test_entries_below_the_hbm_bar_name_their_binding():
+    """A roofline entry under 0.4 of HBM peak carries the counter-derived bound."""
+    e = B.roofline_entry("rollout", "LeeLanded", 4096, 1.62, B.RING)
+    assert e["frac"] < 0.4 and e["binding"] == "valu-issue"
+    assert B.compact_roofline(e)["binding"] == "valu-issue"
+    big = B.roofline_entry("step", "LeeLanded", 4194304, 126.0)
+    assert big["frac"] > 0.4 and "binding" not in big
+    est = B.roofline_entry("rollout", "QuadTracking", 16777216, 1059.0, B.RING)
+    assert est["frac"] < 0.4 and est["binding"] == "valu" and est["issue"]["chip_valu_frac"] > 0.5
