@@ -677,6 +677,8 @@ def compact_line(out):
             row["per_step_kernel_us"] = c["per_step_launch"]["roofline"].get("kernel_us")
         if rf.get("issue"):
             row["valu_issue_frac"] = rf["issue"].get("valu_issue_frac")
+        if rf.get("binding"):
+            row["binding"] = rf["binding"]
         rows.append(row)
     if rows:
         line["configs"] = rows
@@ -687,6 +689,8 @@ def compact_line(out):
             kind = "rollout" if e["kernel"] == "quad_rollout_kernel" or e.get("steps_per_rollout") else "step"
             large[f"{task}/{kind}/{e['num_envs']}"] = {"frac": e.get("frac"),
                                                        "frac_from_rocprof_avg": e.get("frac_from_rocprof_avg")}
+            if e.get("binding"):
+                large[f"{task}/{kind}/{e['num_envs']}"]["binding"] = e["binding"]
     if large:
         line["large_n"] = large
     cpu = out.get("cpu_baseline")
