@@ -458,17 +458,25 @@ class Runner:
             self.plan(k)
             done += k
 
-    def timed(self, steps, world, fused=True):
-        """Wall seconds (max over ranks) and GPU us per step from HIP events on the step stream."""
-        dev = self.dev
+    def setup_timing(self, steps, fused=True):
+        """Everything ``timed`` needs that is not the steps, done BEFORE the warmup so that the warmup's launches
+        are the GPU's last work before the region (no idle gap of host setup in between): the rollout plans and
+        the two timing events (the process's first hipEventCreate costs ~85 us of host time), recorded once (raw
+        hipEventRecord: HipEvents; torch's events if torch's HIP runtime library cannot be opened)."""
         if fused:
             self.prepare(steps)
-        # The events are created (the process's first hipEventCreate costs ~85 us of host time) and recorded
-        # once before the region; the region re-records them (raw hipEventRecord: HipEvents; torch's
-        # events if torch's HIP runtime library cannot be opened).
-        ev = HipEvents(dev) if HipEvents.available() else TorchEvents()
-        ev.record(0)
-        ev.record(1)
+        self.ev = HipEvents(self.dev) if HipEvents.available() else TorchEvents()
+        self.ev.record(0)
+        self.ev.record(1)
+
+    def timed(self, steps, world, fused=True):
+        """Wall seconds (max over ranks) and GPU us per step from HIP events on the step stream (after
+        ``setup_timing`` and the warmup)."""
+        dev = self.dev
+        if getattr(self, "ev", None) is None:
+            self.setup_timing(steps, fused)
+        ev = self.ev
+        self.ev = None
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -517,10 +525,12 @@ class Runner:
 def measure(task, n, dev, seed, rank, world, args, red, with_per_step=True):
     """Headline-style measurement of one config: fused rollouts (timed), then the per-step launch path."""
     run = Runner(task, n, dev, seed, rank, world, red)
+    run.setup_timing(args.steps)
     run.rollouts(max(args.warmup, 1))
     el, gpu_us = run.timed(args.steps, world)
     out = {"value": n * world * args.steps / el, "ms_per_step": el / args.steps * 1e3, "kernel_us": gpu_us}
     if with_per_step:
+        run.setup_timing(args.steps, fused=False)
         run.rollouts(max(args.warmup, 1), fused=False)
         el2, gpu2 = run.timed(args.steps, world, fused=False)
         out["per_step"] = {"value": n * world * args.steps / el2, "ms_per_step": el2 / args.steps * 1e3,
