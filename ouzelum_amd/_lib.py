@@ -208,6 +208,21 @@ def _load():
 
 lib = _load()
 
+_raw_lib = None
+
+
+def raw_function(name: str):
+    """``name`` without ctypes' per-call argument conversion: the same entry point through a second handle of the
+    already-loaded library (``RTLD_NOLOAD``: no second copy) with only its return type set.  Every argument must
+    then be a ctypes instance of the declared C type (``SIGNATURES``), e.g. ``c_void_p`` / ``c_int32``.  For
+    pre-bound hot calls (``QuadVecTask.rollout_plan``): about half the host time of an ``argtypes`` call."""
+    global _raw_lib
+    if _raw_lib is None:
+        _raw_lib = ctypes.CDLL(LIB_PATH, mode=getattr(os, "RTLD_NOLOAD", 4) | getattr(os, "RTLD_NOW", 2))
+    fn = getattr(_raw_lib, name)
+    fn.restype = SIGNATURES[name][0]
+    return fn
+
 
 def check(rc: int, what: str = "") -> None:
     if rc != 0:

@@ -594,10 +594,16 @@ class QuadVecTask:
                 if tuple(tns.shape[:len(shape)]) != shape or tns.dtype != dt:
                     raise ValueError(f"storage {name} must be {shape} {dt}")
             ptrs = [L.ptr(t) for t in storage]
-        fn, env, dr, sp, dev = L.lib.ouz_rollout_stats, self._env, 1 if drain else 0, L.stream_ptr, self._dev_index
+        # the arguments pre-converted once and the entry point called without ctypes' per-call conversion
+        # (L.raw_function): the host time of the first launch of a timed region is on its critical path
+        fn, sp, dev, vp, i32 = L.raw_function("ouz_rollout_stats"), L.stream_ptr, self._dev_index, ctypes.c_void_p, \
+            ctypes.c_int32
+        env, ring_c, len_c, k_c, dr_c = vp(self._env.value), vp(ring_ptr), i32(ring_len), i32(n_steps), \
+            i32(1 if drain else 0)
+        p0, p1, p2, p3 = (vp(p) for p in ptrs)
 
         def run(stats_out_ptr):
-            rc = fn(env, ring_ptr, ring_len, n_steps, ptrs[0], ptrs[1], ptrs[2], ptrs[3], stats_out_ptr, dr, sp(dev))
+            rc = fn(env, ring_c, len_c, k_c, p0, p1, p2, p3, vp(stats_out_ptr), dr_c, vp(sp(dev)))
             if rc:
                 L.check(rc, "ouz_rollout_stats")
         return run

@@ -198,3 +198,19 @@ def test_shipped_library_is_not_instrumented(L):
         assert gone not in src, gone
     shim = open(os.path.join(ROOT, "ouzelum_amd", "_lib.py")).read()
     assert "OUZ_ALLOW_INSTRUMENTED" in shim and "ouz_build_flags" in shim
+
+
+def test_raw_function_is_the_same_entry_point_without_argtypes(L):
+    """rollout_plan's unconverted call goes to the same code as the declared one (one mapped library), and
+    taking it leaves the declared signature of ``L.lib`` untouched."""
+    import ctypes
+    raw = L.raw_function("ouz_rollout_stats")
+    assert raw.argtypes is None and raw.restype is ctypes.c_int
+    decl = L.lib.ouz_rollout_stats
+    assert decl.argtypes is not None and len(decl.argtypes) == 11
+    addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+    assert addr(raw) == addr(decl)
+    # a call with a null env is rejected by the library itself (no GPU involved)
+    vp, i32 = ctypes.c_void_p, ctypes.c_int32
+    rc = raw(vp(None), vp(None), i32(1), i32(1), vp(None), vp(None), vp(None), vp(None), vp(None), i32(1), vp(None))
+    assert rc != 0
