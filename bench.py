@@ -25,8 +25,9 @@ workload from HIP events on its stream; ``roofline_sweep`` repeats the pricing a
 large N, where the state no longer fits the 256 MiB Infinity Cache (at
 4096 envs the whole state is cache-resident, so an HBM fraction there means little).
 ``configs`` carries the other single-GPU BASELINE configs (C, D and E's per-GPU
-shard) measured the same way.  ``cpu_baseline`` times the float64 numpy oracle
-(oracle/quad_oracle.py, "port") on all host cores, before the GPU is touched.
+shard) measured the same way.  ``cpu_baseline`` times, on all host cores and before the GPU is touched, the
+build's own f32 CPU step (``make(sim_device="cpu")``, its ``value``: BASELINE.md §4's vectorised CPU baseline)
+and, as a secondary entry, the float64 numpy oracle (oracle/quad_oracle.py).
 """
 import argparse
 import json
@@ -152,42 +153,62 @@ def host_build_rows(runs, seed, budget_s, cores):
     return rows
 
 
-def cpu_baseline_leg(task, n, seed, budget_s):
-    """The float64 numpy restatement of the step (oracle/quad_oracle.py, "port") in one process per host core
-    of this box (oracle/cpu_bench.py), for every BASELINE config: A (Ouzelum, 64 envs), B and C at
-    N = 64 / 4096 / 8192, D (QuadFault, 8192), E's per-GPU shard (QuadMixed, global ids 0-4095 of 32768),
-    plus the reference-structure per-env estimator loop, one thread.  Beside it (``f32_host``), the build's own
-    f32 host step on the same cores for A-E (BASELINE.md §4.2's vectorised f32 CPU baseline).  Runs before the GPU
-    is initialised (the oracle's worker processes are forked)."""
-    from oracle import cpu_bench as C
-    cores = C.host_cores()
+def cpu_baseline_runs(task, n):
+    """(config, task, envs, env_id_offset, envs_total) of every CPU-baseline run: A (Ouzelum, 64 envs), B and C
+    at N = 64 / 4096 / 8192, D (QuadFault, 8192), E's per-GPU shard (QuadMixed, global ids
+    0-4095 of 32768), and the bench's own workload if it is none of these."""
     sizes = [64, 4096, 8192]
     runs = ([("A", "Ouzelum", 64, 0, 64)] + [("B", "LeeLanded", s, 0, s) for s in sizes]
             + [("C", "QuadTracking", s, 0, s) for s in sizes] + [("D", "QuadFault", 8192, 0, 8192),
                                                                   ("E", "QuadMixed", 4096, 0, 32768)])
     if (task, n) not in {(t, s) for _, t, s, _, _ in runs}:
         runs.insert(0, (TASK_CONFIG.get(task, "-"), task, n, 0, n))
-    per = budget_s * 0.7 / len(runs)
+    return runs
+
+
+def cpu_baseline_record(task, n, cores, host_model, f32, table, ref):
+    """The ``cpu_baseline`` object.  Its ``value`` is the build's own f32 host step at the bench workload (``f32``
+    rows: BASELINE.md §4 timing (2), the one "GPU speedup is quoted against"); the float64 oracle's rows
+    (``table``, the parity checker timed the same way) are a secondary entry, ``oracle_f64``, as is the
+    reference-structure per-env estimator loop (``ref``, BASELINE.md §4 timing (1))."""
+    head = next(r for r in f32 if r["task"] == task and r["num_envs"] == n)
+    rec = {"value": head["value"], "unit": "env-steps/s", "cores": head["cores"], "kind": "port", "leg": "f32_host",
+           "sample": head["sample"] + f"; host {host_model}, {cores} cores available (affinity / cgroup quota / "
+                                      "OMP_NUM_THREADS)",
+           "note": "value: the build's own f32 CPU step (make(sim_device='cpu'), libouzelum_cpu.so: the HIP path's "
+                   "quad_env.h compiled for the host, OpenMP over envs), BASELINE.md §4's vectorised CPU baseline; "
+                   "oracle_f64: the f64 numpy parity oracle on the same cores",
+           "host_cores": cores, "host_model": host_model, "f32_host": f32}
+    if table:
+        o = next(r for r in table if r["task"] == task and r["num_envs"] == n)
+        rec["oracle_f64"] = {"value": o["value"], "unit": "env-steps/s", "cores": o["cores"], "kind": "port",
+                             "sample": o["sample"]}
+        rec["table"] = table
+    if ref:
+        rec["reference_structure_estimator"] = {**ref, "config": "C"}
+    return rec
+
+
+def cpu_baseline_leg(task, n, seed, budget_s):
+    """Every BASELINE config (``cpu_baseline_runs``) on this box's host cores, twice: the build's own f32 host
+    step (``make(sim_device="cpu")``, BASELINE.md §4.2's vectorised f32 CPU restatement: the headline ``value``)
+    and the float64 numpy restatement (oracle/quad_oracle.py, the parity oracle) in one process per core
+    (oracle/cpu_bench.py); plus the reference-structure per-env estimator loop, one thread.  Runs before the GPU is
+    initialised (the oracle's worker processes are forked; the OpenMP host runs follow them)."""
+    from oracle import cpu_bench as C
+    cores = C.host_cores()
+    runs = cpu_baseline_runs(task, n)
+    per = budget_s * 0.45 / len(runs)
     table = []
     for letter, t, s, off, tot in runs:
         r = C.vectorised(t, s, seed=seed, budget_s=per, cores=cores, env_id_offset=off, n_total=tot)
         r["config"] = letter
         table.append(r)
-        print(f"cpu baseline: {t} {s} envs on {r['cores']} cores: {r['value']:.4g} env-steps/s", file=sys.stderr,
-              flush=True)
-    head = next(r for r in table if r["task"] == task and r["num_envs"] == n)
+        print(f"cpu baseline (f64 oracle): {t} {s} envs on {r['cores']} cores: {r['value']:.4g} env-steps/s",
+              file=sys.stderr, flush=True)
     ref = C.reference_structure(n=16, budget_s=budget_s * 0.1)
-    host_runs = [r for r in runs if r[0] in "ABCDE" and (r[0] not in "BC" or r[2] == 4096)]
-    if (task, n) not in {(t, s) for _, t, s, _, _ in host_runs}:
-        host_runs.insert(0, (TASK_CONFIG.get(task, "-"), task, n, 0, n))
-    f32 = host_build_rows(host_runs, seed, budget_s * 0.2 / len(host_runs), cores)
-    return {"value": head["value"], "unit": "env-steps/s", "cores": head["cores"], "kind": "port",
-            "sample": head["sample"] + f"; host {C.host_model()}, {cores} cores available (affinity / cgroup quota "
-                                       "/ OMP_NUM_THREADS)",
-            "leg": "f64 numpy restatement of the step (the parity oracle), one process per core; f32_host: the "
-                   "build's own f32 host step (BASELINE.md §4.2's vectorised f32 CPU restatement) on the same cores",
-            "host_cores": cores, "host_model": C.host_model(), "table": table, "f32_host": f32,
-            "reference_structure_estimator": {**ref, "config": "C"}}
+    f32 = host_build_rows(runs, seed, budget_s * 0.45 / len(runs), cores)
+    return cpu_baseline_record(task, n, cores, C.host_model(), f32, table, ref)
 
 
 # ----------------------------------------------------------------------------------------- GPU side
@@ -705,10 +726,16 @@ def compact_line(out):
         line["large_n"] = large
     cpu = out.get("cpu_baseline")
     if cpu:
-        c = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "sample") if k in cpu}
-        c["by_config"] = {f"{r['config']}/{r['task']}/{r['num_envs']}": r["value"] for r in cpu.get("table", [])}
-        if cpu.get("f32_host"):
-            c["f32_host"] = {f"{r['config']}/{r['task']}/{r['num_envs']}": r["value"] for r in cpu["f32_host"]}
+        c = {k: cpu[k] for k in ("value", "unit", "cores", "kind", "leg", "sample") if k in cpu}
+        key = lambda r: f"{r['config']}/{r['task']}/{r['num_envs']}"  # noqa: E731
+        # by_config: the rows of the headline leg (the f32 host step; the f64 oracle in records before round 5)
+        head_rows = cpu.get("f32_host") if cpu.get("leg") == "f32_host" else cpu.get("table", [])
+        c["by_config"] = {key(r): r["value"] for r in head_rows or []}
+        if cpu.get("oracle_f64"):
+            c["oracle_f64"] = {"value": cpu["oracle_f64"]["value"],
+                               "by_config": {key(r): r["value"] for r in cpu.get("table", [])}}
+        elif cpu.get("f32_host"):
+            c["f32_host"] = {key(r): r["value"] for r in cpu["f32_host"]}
         line["cpu_baseline"] = c
     for k in ("split_timeouts", "detail"):
         if k in out:

@@ -486,6 +486,12 @@ class QuadVecTask:
         outputs copied into ``storage`` rows when given, then the statistics.  Fused or not is the same here."""
         H = L.host_lib()
         n = self.num_envs
+        if stats_out is not None:   # the same checks as episode_stats() and the HIP path, before any step runs
+            if not self.cfg.track_episodes:
+                raise RuntimeError("create the env with track_episodes=True")
+            if (not isinstance(stats_out, torch.Tensor) or stats_out.dtype != torch.float64 or stats_out.numel() < 3
+                    or not stats_out.is_contiguous() or stats_out.device.type != "cpu"):
+                raise ValueError("stats_out must be a contiguous float64 CPU tensor of >= 3")
         if action_ring is None:
             ring, ring_len = (self._zero_actions[None] if self.uses_actions else None), 1
         else:
@@ -509,8 +515,6 @@ class QuadVecTask:
                 rst[k].copy_(self.reset_buf)
                 to[k].copy_(self.timeout_buf)
         if stats_out is not None:
-            if stats_out.dtype != torch.float64 or stats_out.numel() < 3 or stats_out.device.type != "cpu":
-                raise ValueError("stats_out must be a float64 CPU tensor of >= 3")
             L.host_check(H.ouz_host_episode_stats(self._env, L.ptr(stats_out), 1 if drain else 0),
                          "ouz_host_episode_stats")
 
@@ -646,10 +650,12 @@ class QuadVecTask:
                 "step": self.sim_step_count, "task": self.task, "num_envs": self.num_envs, "layout": self._layout()}
 
     def load_state_dict(self, sd, strict=True):
-        """Restore a ``state_dict``.  A checkpoint whose layout marker differs from this env's is refused (its slot
-        order differs: ABI version, slot count or shard offset).  A checkpoint written before the marker existed
-        (no ``layout`` key) is loaded with a warning when its tensor shapes match, or refused if ``strict`` and
-        the shapes do not; ``strict=False`` skips the layout comparison altogether (the caller vouches for it)."""
+        """Restore a ``state_dict``.  Always refused: another task or env count, or state tensors of other shapes.
+        With ``strict`` (the default) the checkpoint's layout marker must equal this env's: a checkpoint of another
+        layout (ABI version, slot count or shard offset: its slot order differs) or without a marker (written before
+        the marker existed, when ABI 2 and 3 had already changed the slot order of the estimator tasks and of the
+        mixed curriculum with the same slot count) is refused.  ``strict=False`` skips the layout comparison and
+        loads such a checkpoint with a warning: the caller vouches that its slot order is this env's."""
         import warnings
         if sd["task"] != self.task or sd["num_envs"] != self.num_envs:
             raise ValueError("checkpoint is for a different task / env count")
@@ -658,12 +664,14 @@ class QuadVecTask:
         if not shapes_match:
             raise ValueError(f"checkpoint state shapes {tuple(sd['fstate'].shape)} / {tuple(sd['istate'].shape)} != "
                              f"this env's {tuple(self.fstate.shape)} / {tuple(self.istate.shape)}")
-        if "layout" not in sd:
-            warnings.warn("env checkpoint without a layout marker (written before ABI 3's marker): loaded because "
-                          "its shapes match; its slot order is assumed to be this env's", stacklevel=2)
-        elif strict and sd["layout"] != self._layout():
-            raise ValueError(f"checkpoint state layout {sd.get('layout')} != this env's {self._layout()} "
-                             "(slot order differs: ABI version, slot count or shard offset)")
+        if sd.get("layout") != self._layout():
+            what = "without a layout marker" if "layout" not in sd else f"of layout {sd['layout']}"
+            if strict:
+                raise ValueError(f"checkpoint state {what} != this env's {self._layout()} (its slot order may differ: "
+                                 "ABI version, slot count or shard offset); load_state_dict(sd, strict=False) loads "
+                                 "it anyway")
+            warnings.warn(f"env checkpoint {what} loaded with strict=False: its slot order is assumed to be this "
+                          "env's", stacklevel=2)
         self.fstate.copy_(sd["fstate"])
         self.istate.copy_(sd["istate"])
         self.obs_buf.copy_(sd["obs"])

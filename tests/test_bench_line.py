@@ -53,6 +53,26 @@ def test_compact_line_under_limit_and_round_trips(full):
     assert any(k.endswith("/16777216") for k in d["large_n"])
 
 
+def test_cpu_baseline_headline_is_the_f32_host_step(full):
+    """"GPU speedup is quoted against timing (2)", the build's own vectorised f32 CPU step -- so
+    ``cpu_baseline.value`` is the f32 host row of the bench workload, and the f64 oracle is a secondary entry
+    (VERDICT r04 item 3).  B and C carry N = 64 / 4096 / 8192 rows on both legs."""
+    runs = B.cpu_baseline_runs("LeeLanded", 4096)
+    assert {(t, s) for c, t, s, _, _ in runs if c in "BC"} == {(t, s) for t in ("LeeLanded", "QuadTracking")
+                                                                for s in (64, 4096, 8192)}
+    row = lambda c, t, s, v, k: {"config": c, "task": t, "num_envs": s, "value": v, "cores": 16, "sample": k}  # noqa
+    f32 = [row(c, t, s, 6.6e7 + s, "f32") for c, t, s, _, _ in runs]
+    table = [row(c, t, s, 5.4e6 + s, "f64") for c, t, s, _, _ in runs]
+    rec = B.cpu_baseline_record("LeeLanded", 4096, 16, "test cpu", f32, table, {"value": 2.2e3})
+    assert rec["value"] == 6.6e7 + 4096 and rec["leg"] == "f32_host" and rec["kind"] == "port"
+    assert rec["oracle_f64"]["value"] == 5.4e6 + 4096
+    d = json.loads(B.compact_line({**full, "cpu_baseline": rec}))
+    cpu = d["cpu_baseline"]
+    assert cpu["value"] == rec["value"] and cpu["leg"] == "f32_host"
+    assert cpu["by_config"]["B/LeeLanded/4096"] == 6.6e7 + 4096 and len(cpu["by_config"]) == len(runs)
+    assert cpu["oracle_f64"]["value"] == 5.4e6 + 4096 and len(cpu["oracle_f64"]["by_config"]) == len(runs)
+
+
 def test_compact_line_drops_optional_parts_rather_than_overflow(full):
     big = dict(full)
     big["configs"] = full["configs"] * 40            # absurdly many rows

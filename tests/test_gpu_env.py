@@ -245,16 +245,20 @@ def test_state_dict_roundtrip(ouz):
         env.step(None)
     assert torch.equal(a, env.fstate)
     # a checkpoint of another slot layout is refused: another shard offset of the mixed
-    # curriculum; a layout-less (round-1 style) checkpoint with matching shapes loads with a warning,
-    # one with other shapes is refused
+    # curriculum; a layout-less (round-1 style) checkpoint is refused unless the caller opts in with strict=False,
+    # then it loads with a warning; one with other shapes is refused either way
     bad = dict(sd)
     bad.pop("layout")
-    with pytest.warns(UserWarning, match="layout marker"):
+    env.fstate.zero_()
+    with pytest.raises(ValueError, match="layout marker"):
         env.load_state_dict(bad)
+    with pytest.warns(UserWarning, match="layout marker"):
+        env.load_state_dict(bad, strict=False)
     assert torch.equal(env.fstate, sd["fstate"])
     bad["fstate"] = sd["fstate"][:-1]
-    with pytest.raises(ValueError):
-        env.load_state_dict(bad)
+    for strict in (True, False):
+        with pytest.raises(ValueError):
+            env.load_state_dict(bad, strict=strict)
     m0 = ouz.make(seed=1, task="QuadMixed", num_envs=1344, sim_device="cuda:0", env_id_offset=0,
                   num_envs_total=4032)
     m1 = ouz.make(seed=1, task="QuadMixed", num_envs=1344, sim_device="cuda:0", env_id_offset=1344,

@@ -181,3 +181,12 @@ def test_host_vectask_surface():
         env.pre_physics()
     with pytest.raises(ValueError):
         env.step(torch.zeros((n + 1, 4)))
+    # rollout statistics need track_episodes and a contiguous f64 tensor, checked before any step runs (as the
+    # HIP path and episode_stats() do)
+    with pytest.raises(ValueError):
+        env.rollout(ring, 4, stats_out=torch.zeros(3, dtype=torch.float32))
+    untracked = ouzelum_amd.make(seed=1, task="QuadFault", num_envs=n, sim_device="cpu")
+    step0 = untracked.sim_step_count
+    with pytest.raises(RuntimeError, match="track_episodes"):
+        untracked.rollout(ring, 4, stats_out=torch.zeros(3, dtype=torch.float64))
+    assert untracked.sim_step_count == step0
