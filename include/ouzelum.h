@@ -60,8 +60,10 @@
 extern "C" {
 #endif
 
-#define OUZ_ABI_VERSION 3   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
-                               3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots */
+#define OUZ_ABI_VERSION 4   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
+                               3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots;
+                               4: physical domain randomisation (ouz_dr_physical, OUZ_I_RAND_STEP), DR noise
+                                  frequency (ouz_dr_noise.frequency) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -145,7 +147,7 @@ enum {
   OUZ_F_WAYPOINT = 91,  /* target_waypoints (3)                                 */
   OUZ_F_PLAT = 94,      /* landing-platform xy (2)                              */
   OUZ_F_TRAJ_SD = 96,   /* trajectory scale * direction (1)                     */
-  OUZ_F_DR = 97,        /* DR scales: mass, inertia, thrust (3)                 */
+  OUZ_F_DR = 97,        /* DR scales of the nominal mass, inertia xx/yy, motor constant (3)        */
   OUZ_F_FAULT_ETA = 100,/* faulty-rotor efficiency (1)                          */
   OUZ_F_EP_RET = 101,   /* running episode return (RecordEpisodeStatisticsTorch) */
   OUZ_F_EP_SUM = 102,   /* sum of returns of episodes finished since last drain  */
@@ -163,7 +165,9 @@ enum {
   OUZ_I_LANDINGS = 6,   /* per-env landing count (self.Landoa summed)           */
   OUZ_I_EP_CNT = 7,     /* episodes finished since last drain                   */
   OUZ_I_EP_LEN = 8,     /* summed lengths of those episodes (info["l"])          */
-  OUZ_I_COUNT = 9
+  OUZ_I_RAND_STEP = 9,  /* step of the env's last physical randomization (-1: never); the reference's
+                           randomize_buf (vec_task.py:275,560-563) is step - this                  */
+  OUZ_I_COUNT = 10
 };
 
 typedef struct ouz_config {
@@ -197,14 +201,14 @@ typedef struct ouz_buffers {
   uint8_t* timeouts;        /* [num_envs] bool time_outs                         */
 } ouz_buffers;
 
-/* VecTask domain-randomisation noise on observations / actions (tasks/base/
- * vec_task.py:576-646 "observations" / "actions" entries; applied in step() before
- * the clamps, :323-325,352-353).  noise = corr * b_c + a_c + fresh * b + a (gaussian,
- * a = mu, b = the reference's "var", used there as a standard deviation) or
- * corr * (hi_c - lo_c) + lo_c + U[0,1) * (hi - lo) + lo (uniform); corr ~ N(0,1) is drawn
- * once per env element and kept (the reference's params['corr']); x + noise (additive) or
- * x * noise (scaling).  schedule: 0 none, 1 linear over schedule_steps, 2 constant (off
- * until schedule_steps), evaluated at the current step. */
+/* VecTask domain-randomisation noise on observations / actions (tasks/base/vec_task.py:576-646 "observations" /
+ * "actions" entries; applied in step() before the clamps, :323-325,352-353).  noise = corr * b_c + a_c + fresh * b + a
+ * (gaussian, a = mu, b = the reference's "var", used there as a standard deviation) or
+ * corr * (hi_c - lo_c) + lo_c + U[0,1) * (hi - lo) + lo (uniform); x + noise (additive) or x * noise (scaling).
+ * The parameters are re-derived every `frequency` steps (do_nonenv_randomize, :559,577): at step t they are those of
+ * the epoch e = t - t % frequency, the schedule (0 none, 1 linear over schedule_steps, 2 constant: off until
+ * schedule_steps) is evaluated at e, and corr ~ N(0,1), drawn per env element, is redrawn at every epoch (each
+ * re-derivation builds a new params dict without 'corr', :610-620).  frequency <= 1: every step. */
 typedef struct ouz_dr_noise {
   int32_t distribution;     /* 0 off, 1 gaussian, 2 uniform                       */
   int32_t operation;        /* 0 additive, 1 scaling                              */
@@ -212,7 +216,40 @@ typedef struct ouz_dr_noise {
   float range_correlated[2];
   int32_t schedule;         /* 0 none, 1 linear, 2 constant                       */
   int32_t schedule_steps;
+  int32_t frequency;        /* dr_params["frequency"] (default 1)                 */
+  int32_t reserved;
 } ouz_dr_noise;
+
+/* Physical domain randomisation: VecTask.apply_randomizations' actor_params of the drone actor ("Drone",
+ * ekf_lee_landed.py:242; vec_task.py:680-756) on the build's lumped rigid body.  At the lazy reset
+ * of an env (reset_idx -> apply_randomizations, e.g. ant.py:246-248) whose randomize_buf = step - OUZ_I_RAND_STEP
+ * >= frequency (vec_task.py:547-563; an env never randomized always is), each enabled parameter draws one sample
+ * as dr_utils.generate_random_samples does (:71-133: the schedule at the current step scales the range, additive
+ * ranges toward 0, scaling ranges toward 1; uniform lo + U(hi - lo), loguniform exp(U(log lo, log hi)), gaussian
+ * mu + var * N(0, 1)) from the counter RNG, and sets the value from the nominal one as apply_random_samples does
+ * (:148-205: nominal * sample or nominal + sample, never cumulative).  setup_only: only at the env's first
+ * randomization.  Stored per env as scales of the nominal value (OUZ_F_DR). */
+typedef struct ouz_dr_param {
+  int32_t distribution;     /* 0 off, 1 gaussian, 2 uniform, 3 loguniform         */
+  int32_t operation;        /* 0 additive, 1 scaling                              */
+  float range[2];           /* (mu, var) or (lo, hi)                              */
+  int32_t schedule;         /* 0 none, 1 linear, 2 constant                       */
+  int32_t schedule_steps;
+  int32_t setup_only;
+  int32_t reserved;
+} ouz_dr_param;
+/* parameters: rigid_body_properties.mass (2.064 kg), rigid_body_properties.inertia (diag(0.0293, 0.0293, 0.0440):
+ * scaling multiplies the tensor, additive adds the sample to each diagonal entry), and the rotors' motorConstant
+ * (assets/x500/model.sdf:523, 8.54858e-6: every rotor's thrust scales with it) */
+#define OUZ_DRP_MASS 0
+#define OUZ_DRP_INERTIA 1
+#define OUZ_DRP_MOTOR_CONSTANT 2
+#define OUZ_DRP_COUNT 3
+typedef struct ouz_dr_physical {
+  int32_t frequency;        /* dr_params["frequency"] (default 1)                 */
+  int32_t reserved;
+  ouz_dr_param param[OUZ_DRP_COUNT];
+} ouz_dr_physical;
 
 typedef struct ouz_task_info {
   int32_t max_episode_length;
@@ -300,6 +337,10 @@ int ouz_step_n_stats(ouz_env* env, const float* action_ring, int32_t ring_len, i
 int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity);
 /* target 0 = observations, 1 = actions; dr == NULL or distribution 0 disables. */
 int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr);
+/* Physical DR of every env of this env object (all tasks of a curriculum), replacing the task default (QuadTracking:
+ * mass / inertia / motor constant scaling ~ U(dr_lo, dr_hi) at every reset; the other tasks: none).  dr == NULL or
+ * every distribution 0: off.  Takes effect at the next launch. */
+int ouz_set_dr_physical(ouz_env* env, const ouz_dr_physical* dr);
 int64_t ouz_get_step(const ouz_env* env);
 int ouz_set_step(ouz_env* env, int64_t step);
 

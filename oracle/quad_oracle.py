@@ -555,16 +555,26 @@ def _normal_from(a, b, second):
     return r * (np.sin(2 * math.pi * u2) if second else np.cos(2 * math.pi * u2))
 
 
+def dr_schedule(sched, sched_steps, step):
+    """Schedule scaling of a DR range at ``step`` (vec_task.py:584-589, dr_utils.py:82-87), in float32 as the
+    kernel evaluates it."""
+    if sched == 1:
+        return float(np.float32(min(float(step), float(sched_steps))) / np.float32(sched_steps))
+    if sched == 2:
+        return 0.0 if step < sched_steps else 1.0
+    return 1.0
+
+
 def dr_noise_apply(x, p, seed, env_ids, step, stream):
-    """One noise_lambda call.  p: dict with distribution/operation/range/range_correlated/
-    schedule/schedule_steps (the reference's dr_params entry, names mapped to ints)."""
+    """One noise_lambda call.  p: dict with distribution/operation/range/range_correlated/schedule/schedule_steps/
+    frequency (the reference's dr_params entry, names mapped to ints).  The parameters are those of the epoch
+    e = step - step % frequency (do_nonenv_randomize re-derives them every ``frequency`` steps, vec_task.py:559,
+    577-646): schedule at e, corr redrawn at every epoch (a new params dict has no 'corr', :610-615)."""
     if not p or p.get("distribution", 0) == 0:
         return x
-    s = 1.0
-    if p["schedule"] == 1:
-        s = min(step, p["schedule_steps"]) / p["schedule_steps"]
-    elif p["schedule"] == 2:
-        s = 0.0 if step < p["schedule_steps"] else 1.0
+    freq = int(p.get("frequency", 1))
+    ep = step - step % freq if freq > 1 else step
+    s = dr_schedule(p["schedule"], p["schedule_steps"], ep)
     a, b = (float(np.float32(v)) for v in p["range"])
     ac, bc = (float(np.float32(v)) for v in p["range_correlated"])
     add, gauss = p["operation"] == 0, p["distribution"] == 1
@@ -578,7 +588,7 @@ def dr_noise_apply(x, p, seed, env_ids, step, stream):
     d = out.shape[1]
     for g in range((d + 3) // 4):
         f = rng.draw_u32(seed, env_ids, step, stream, g)
-        c = rng.draw_u32(seed, env_ids, rng.INIT_STEP, stream, g)
+        c = rng.draw_u32(seed, env_ids, ep, stream, 64 + g)
         for k in range(4):
             e = g * 4 + k
             if e >= d:
@@ -591,6 +601,45 @@ def dr_noise_apply(x, p, seed, env_ids, step, stream):
                 n = corr * (bc - ac) + ac + rng.u32_to_unit_f32(f[k]).astype(np.float64) * (b - a) + a
             out[:, e] = out[:, e] + n if add else out[:, e] * n
     return out
+
+
+# ---------------------------------------------------------------------------
+# Physical DR (a22): VecTask.apply_randomizations' actor_params (vec_task.py:547-563,680-756) of the drone's lumped
+# body, samples as dr_utils.generate_random_samples (:71-133), values as apply_random_samples (:148-205)
+# ---------------------------------------------------------------------------
+DRP_DIST = {"gaussian": 1, "uniform": 2, "loguniform": 3}
+MOTOR_CONSTANT = 8.54858e-06     # assets/x500/model.sdf:523
+
+
+def dr_phys_default(lo=0.9, hi=1.1):
+    """QuadTracking's default: mass, inertia and motor-constant scaling ~ U(lo, hi) at every reset."""
+    prm = {"distribution": 2, "operation": 1, "range": (lo, hi), "schedule": 0, "schedule_steps": 0, "setup_only": 0}
+    return {"frequency": 1, "params": [dict(prm) for _ in range(3)]}
+
+
+def dr_sample(p, u, u2, step):
+    """generate_random_samples with the counter RNG: u (and u2, the gaussian's Box-Muller partner) uint32 draws.
+    The range and schedule in float32, as the kernel forms them."""
+    s = np.float32(dr_schedule(p["schedule"], p["schedule_steps"], step))
+    a, b = np.float32(p["range"][0]), np.float32(p["range"][1])
+    one = np.float32(1.0)
+    if p["operation"] == 0:
+        a, b = a * s, b * s
+    elif p["distribution"] == 1:
+        b, a = b * s, a * s + (one - s)
+    else:
+        a, b = a * s + (one - s), b * s + (one - s)
+    if p["distribution"] == 1:
+        return float(a) + float(b) * _normal_from(u, u2, False)
+    if p["distribution"] == 3:
+        return np.exp(rng.uniform_f32(u, float(np.log(a).astype(np.float32)), float(np.log(b).astype(np.float32)))
+                      .astype(np.float64))
+    return rng.uniform_f32(u, float(a), float(b)).astype(np.float64)
+
+
+def dr_scale(p, sample, nominal):
+    """apply_random_samples' new value (:186-188) as a scale of the nominal one."""
+    return (nominal + sample) / nominal if p["operation"] == 0 else sample
 
 
 # ---------------------------------------------------------------------------
@@ -667,6 +716,7 @@ class EnvConfig:
     thrust_max: float = 2000.0   # ouzelum.py:91
     thrust_rate: float = 2000.0  # ouzelum.py:237
     max_episode_length: int = 0  # 0 -> task default
+    dr_phys: dict | None = None  # physical DR ({frequency, params: [mass, inertia, motor constant]}); None: task default
     dr_obs: dict | None = None   # VecTask DR noise on observations / actions (dr_noise_apply's p)
     dr_act: dict | None = None
 
@@ -721,7 +771,15 @@ class OracleEnv:
         self.traj_type = np.zeros(n, np.int64)
         self.traj_sd = f()
         self.traj_idx = np.zeros(n, np.int64)
-        self.dr = np.ones((n, 3), dtype)         # mass, inertia, thrust scales
+        self.dr = np.ones((n, 3), dtype)         # mass, inertia (xx / yy), motor-constant scales
+        self.rand_step = np.full(n, -1, np.int64)  # step of the last physical randomization (-1: never)
+        if cfg.dr_phys is not None:              # set for every env of the env object (ouz_set_dr_physical)
+            on = any(q["distribution"] for q in cfg.dr_phys["params"])
+            self.dr_phys = cfg.dr_phys if on else None
+            self.dr_on = np.full(n, on)
+        else:                                    # the task default: QuadTracking's envs
+            self.dr_phys = dr_phys_default(cfg.dr_lo, cfg.dr_hi)
+            self.dr_on = np.array([self.specs[t].dr for t in self.task_ids], bool)
         self.fault_rotor = np.zeros(n, np.int64)
         self.fault_eta = np.ones(n, dtype)
         self.fault_onset = np.zeros(n, np.int64)
@@ -786,11 +844,20 @@ class OracleEnv:
         self.reset_buf[rst] = 0
         self.landings[rst] += self.land_flag[rst]
         self.land_flag[rst] = 0
-        if any(s.dr for s in self.specs.values()):
+        if self.dr_on.any():   # apply_randomizations at reset (vec_task.py:547-563)
+            ph = self.dr_phys
+            first = self.rand_step < 0
+            due = rst & self.dr_on & (first | (t - self.rand_step >= ph["frequency"]))
             wd = rng.draw_u32(cfg.seed, ids, t, rng.RNG_DR)
-            dr = np.stack([rng.uniform_f32(wd[k], cfg.dr_lo, cfg.dr_hi) for k in range(3)], 1)
-            m = rst & np.array([self.specs[tt].dr for tt in self.task_ids])
-            self.dr[m] = dr[m]
+            we = rng.draw_u32(cfg.seed, ids, t, rng.RNG_DR, 1)
+            for k, nominal in enumerate((MASS, INERTIA[0], MOTOR_CONSTANT)):
+                q = ph["params"][k]
+                if not q["distribution"]:
+                    continue
+                sel = due & (first | (not q.get("setup_only", 0)))
+                val = dr_scale(q, dr_sample(q, wd[k], we[k], t), nominal)
+                self.dr[sel, k] = np.broadcast_to(val, (n,))[sel]
+            self.rand_step[due] = t
         if any(s.fault for s in self.specs.values()):
             wf = rng.draw_u32(cfg.seed, ids, t, rng.RNG_FAULT)
             m = rst & np.array([self.specs[tt].fault for tt in self.task_ids])
@@ -814,6 +881,11 @@ class OracleEnv:
         # ---- physics (vec_task.py:332-335 -> build-defined integrator) ----
         mass = MASS * self.dr[:, 0]
         inertia = INERTIA[None, :] * self.dr[:, 1:2]
+        ph = self.dr_phys
+        if ph is not None and ph["params"][1]["distribution"] and ph["params"][1]["operation"] == 0:
+            # additive inertia: the same sample on each diagonal entry, so the zz scale follows from the xx scale
+            inertia = inertia.copy()
+            inertia[:, 2] = INERTIA[2] * (1.0 + (self.dr[:, 1] - 1.0) * INERTIA[0] / INERTIA[2])
         deck_on = np.array([self.specs[tt].target_mode != TGT_GOAL for tt in self.task_ids])
         self.p, self.q, self.v, self.w = integrate(self.p, self.q, self.v, self.w, f_b, tau_b,
                                                    mass.astype(dtype), inertia.astype(dtype), dt, cfg.substeps,
@@ -865,6 +937,8 @@ class OracleEnv:
             eff[rows, k[rows]] *= self.fault_eta[m][rows]
         eff[rst[m]] = 0.0
         th[rst[m]] = 0.0
+        if self.dr_on[m].any():   # the rotors' motor-constant scale (physical DR)
+            eff = np.where(self.dr_on[m][:, None], eff * self.dr[m, 2:3], eff)
         self.thrust[m] = th
         tot = eff.sum(1)
         fb = np.zeros((m.sum(), 3), self.dt_)

@@ -25,8 +25,8 @@ class OuzelumError(RuntimeError):
 
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
-ABI_VERSION = 3
-LAYOUT_VERSION = 3  # the ABI version whose state-slot rules (include/ouzelum.h "State slots") the layout follows
+ABI_VERSION = 4
+LAYOUT_VERSION = 4  # the ABI version whose state-slot rules (include/ouzelum.h "State slots") the layout follows
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
 POMDP_NONE, POMDP_FLICKER, POMDP_NOISE, POMDP_FLICKER_NOISE = range(4)
@@ -39,8 +39,11 @@ F_P, F_Q, F_V, F_W, F_TARGET, F_PREV_V, F_THRUST = 0, 3, 7, 10, 13, 16, 19
 F_EKF_Q, F_EKF_P, F_PV_X, F_PV_P, F_WAYPOINT, F_PLAT, F_TRAJ_SD, F_DR, F_FAULT_ETA = 23, 27, 37, 46, 91, 94, 96, 97, 100
 F_EP_RET, F_EP_SUM, F_PLAT_HEADING = 101, 102, 103
 F_COUNT = 104
-I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT, I_EP_LEN = range(9)
-I_COUNT = 9
+I_PROGRESS, I_TRAJ_TYPE, I_TRAJ_IDX, I_FAULT_ROTOR, I_FAULT_ONSET, I_LAND_FLAG, I_LANDINGS, I_EP_CNT, I_EP_LEN, \
+    I_RAND_STEP = range(10)
+I_COUNT = 10
+DRP_MASS, DRP_INERTIA, DRP_MOTOR_CONSTANT = range(3)
+DRP_COUNT = 3
 BUILD_STAMPS, BUILD_TEMPORAL_STORES = 1, 2  # ouz_build_flags bits
 TILE = 64  # OUZ_TILE: state is [tiles][fields][64] (ouzelum.h OUZ_FIDX)
 
@@ -64,7 +67,17 @@ class OuzConfig(ctypes.Structure):
 class OuzDrNoise(ctypes.Structure):
     _fields_ = [("distribution", ctypes.c_int32), ("operation", ctypes.c_int32), ("range", ctypes.c_float * 2),
                 ("range_correlated", ctypes.c_float * 2), ("schedule", ctypes.c_int32),
-                ("schedule_steps", ctypes.c_int32)]
+                ("schedule_steps", ctypes.c_int32), ("frequency", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class OuzDrParam(ctypes.Structure):
+    _fields_ = [("distribution", ctypes.c_int32), ("operation", ctypes.c_int32), ("range", ctypes.c_float * 2),
+                ("schedule", ctypes.c_int32), ("schedule_steps", ctypes.c_int32), ("setup_only", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class OuzDrPhysical(ctypes.Structure):
+    _fields_ = [("frequency", ctypes.c_int32), ("reserved", ctypes.c_int32), ("param", OuzDrParam * 3)]
 
 
 class OuzBuffers(ctypes.Structure):
@@ -112,6 +125,7 @@ SIGNATURES = {
     "ouz_step_n_stats": (_I, [_P, _P, _I, _I, _P, _I, _P]),
     "ouz_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
+    "ouz_set_dr_physical": (_I, [_P, ctypes.POINTER(OuzDrPhysical)]),
     "ouz_get_step": (_I64, [_P]),
     "ouz_set_step": (_I, [_P, _I64]),
     "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),
@@ -146,6 +160,7 @@ HOST_SIGNATURES = {
     "ouz_host_episode_stats": (_I, [_P, _P, _I]),
     "ouz_host_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_host_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
+    "ouz_host_set_dr_physical": (_I, [_P, ctypes.POINTER(OuzDrPhysical)]),
     "ouz_host_get_step": (_I64, [_P]),
     "ouz_host_set_step": (_I, [_P, _I64]),
 }

@@ -149,6 +149,15 @@ struct EnvConsts {
   float inv_mass, inv_ixx, inv_iyy, inv_izz;
 };
 
+// Physical domain randomisation as the step reads it (include/ouzelum.h ouz_dr_physical): the ABI parameters and
+// what the host derives from them once.
+struct PhysDr {
+  ouz_dr_physical p;
+  int32_t need_last;     // frequency > 1 or a setup_only parameter: the reset reads the env's OUZ_I_RAND_STEP
+  int32_t gauss;         // a gaussian parameter: the reset draws a second Philox block for its Box-Muller pairs
+  int32_t inertia_add;   // additive inertia: the zz scale follows from the xx scale (the same sample on each axis)
+};
+
 struct StepArgs {
   float* f;
   int32_t* iv;
@@ -180,6 +189,7 @@ struct StepArgs {
   int32_t trace_env, trace_cap;
   EnvConsts c;
   TaskParams tp[3];            // by tp_slot(task): the configured task, or the three curriculum tasks
+  PhysDr pdr;                  // physical DR of the tasks whose TaskParams.dr is set
 };
 
 // Task-parameter slot: a single-task env fills only its task's slot, the mixed curriculum the slots of
@@ -281,14 +291,23 @@ OUZ_DEV float normal_from(uint32_t a, uint32_t b, bool second) {
   return second ? r * sn : r * cs;
 }
 
-// D values of env gid (D <= 16): noise drawn from `stream`, subs 0..3 fresh (step-keyed), corr at INIT_STEP
+// Schedule scaling of a DR range at `step` (vec_task.py:584-589, dr_utils.py:82-87)
+OUZ_DEV float dr_schedule(int32_t sched, int32_t sched_steps, uint32_t step) {
+  if (sched == 1) return fminf((float)step, (float)sched_steps) / (float)sched_steps;
+  if (sched == 2) return step < (uint32_t)sched_steps ? 0.0f : 1.0f;
+  return 1.0f;
+}
+
+// D values of env gid (D <= 16): noise drawn from `stream`.  The parameters are those of the epoch
+// e = step - step % frequency (the apply_randomizations call that last re-derived them, vec_task.py:559,577-646):
+// the schedule is evaluated at e and the correlated draw corr (subs 64..) is keyed by e, so it is redrawn at every
+// epoch (a new params dict has no 'corr', :610-615); the fresh draws (subs 0..3) are keyed by the step.
 template <int D>
 OUZ_DEV void dr_noise_apply(float* x, const ouz_dr_noise& p, uint64_t seed, uint32_t gid,
                                                uint32_t step, uint32_t stream) {
   if (p.distribution == 0) return;
-  float s = 1.0f;                                                        // schedule (vec_task.py:584-589)
-  if (p.schedule == 1) s = fminf((float)step, (float)p.schedule_steps) / (float)p.schedule_steps;
-  else if (p.schedule == 2) s = step < (uint32_t)p.schedule_steps ? 0.0f : 1.0f;
+  const uint32_t ep = p.frequency > 1 ? step - step % (uint32_t)p.frequency : step;
+  const float s = dr_schedule(p.schedule, p.schedule_steps, ep);
   float a = p.range[0], b = p.range[1], ac = p.range_correlated[0], bc = p.range_correlated[1];
   const bool add = p.operation == 0, gauss = p.distribution == 1;
   if (add) {
@@ -298,10 +317,9 @@ OUZ_DEV void dr_noise_apply(float* x, const ouz_dr_noise& p, uint64_t seed, uint
   } else {                                                               // :629-633
     a = a * s + (1.0f - s); b = b * s + (1.0f - s); ac = ac * s + (1.0f - s); bc = bc * s + (1.0f - s);
   }
-  // Keep the correlated (step-independent) draws inside this rarely enabled branch: they are loop
-  // invariant in the fused rollout, and loop-invariant code motion hoisted them with their Box-Muller
-  // log / sincos out of the step loop and speculated them unconditionally, ~1500 instructions (~5000
-  // cycles) before the first step of every launch whether or not DR noise was on
+  // Keep the correlated draws inside this rarely enabled branch: loop-invariant code motion hoisted them with
+  // their Box-Muller log / sincos out of the fused rollout's step loop and speculated them unconditionally,
+  // ~1500 instructions (~5000 cycles) before the first step of every launch whether or not DR noise was on
   // (scripts/stamp_rollout.py prologue, LeeLanded 8520 -> 3316 cycles).
 #ifndef OUZ_HOST
   __asm__ volatile("" : "+v"(gid));
@@ -310,7 +328,7 @@ OUZ_DEV void dr_noise_apply(float* x, const ouz_dr_noise& p, uint64_t seed, uint
 #pragma unroll
   for (int g = 0; g < (D + 3) / 4; ++g) {
     const U4 f = draw(seed, gid, step, stream, (uint32_t)g);
-    const U4 c = draw(seed, gid, INIT_STEP, stream, (uint32_t)g);
+    const U4 c = draw(seed, gid, ep, stream, 64u + (uint32_t)g);
     const uint32_t fw[4] = {f.x, f.y, f.z, f.w}, cw[4] = {c.x, c.y, c.z, c.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -324,6 +342,26 @@ OUZ_DEV void dr_noise_apply(float* x, const ouz_dr_noise& p, uint64_t seed, uint
     }
   }
 }
+
+// ---------------------------------------------------------------------------
+// Physical DR (include/ouzelum.h ouz_dr_physical): one sample of dr_utils.generate_random_samples (:71-133) with the
+// counter RNG -- u (and u2, the gaussian's Box-Muller partner) two draws of the env -- and the env's scale of the
+// nominal value after apply_random_samples (:186-188: nominal * sample, or nominal + sample).
+// ---------------------------------------------------------------------------
+OUZ_DEV float dr_sample(const ouz_dr_param& p, uint32_t u, uint32_t u2, uint32_t step) {
+  const float s = dr_schedule(p.schedule, p.schedule_steps, step);
+  float a = p.range[0], b = p.range[1];
+  if (p.operation == 0) { a *= s; b *= s; }                                  // additive: toward 0
+  else if (p.distribution == 1) { b *= s; a = a * s + (1.0f - s); }          // scaling gaussian: mu toward 1
+  else { a = a * s + (1.0f - s); b = b * s + (1.0f - s); }                   // scaling (log)uniform: toward 1
+  if (p.distribution == 1) return a + b * normal_from(u, u2, false);         // np.random.normal(mu, var)
+  if (p.distribution == 3) return expf(uniform_f32(u, logf(a), logf(b)));    // exp(np.random.uniform(log lo, log hi))
+  return uniform_f32(u, a, b);                                               // np.random.uniform(lo, hi)
+}
+OUZ_DEV float dr_scale(const ouz_dr_param& p, float sample, float nominal) {
+  return p.operation == 0 ? (nominal + sample) / nominal : sample;
+}
+constexpr float kMotorConstant = 8.54858e-06f;   // assets/x500/model.sdf:523 (T = k_f w^2 per rotor)
 
 // Wave-tiled SoA (include/ouzelum.h OUZ_FIDX): a wave's fields are contiguous
 // 256-byte rows, field f at offset f*256 from the wave's tile base.  The tile base is
@@ -437,6 +475,7 @@ struct EnvRegs {
   int32_t frot, fonset;           // fault
   float eta;
   float dr_m, dr_i, dr_t;         // domain randomisation scales
+  int32_t rand_step;              // step of the last physical randomization (stored with the scales)
   V3 prev_v, wp;                  // CTRL_LEE_EST
   EkfQ eq;
   float eP[10], px[9], pP[45];
@@ -552,7 +591,10 @@ OUZ_DEV void env_store(const StepArgs& a, int i, const TaskParams& tp, const Env
   }
   if (S.landings_add) OUZ_ACC_ADD(&S.T.iv[(uint32_t)OUZ_I_LANDINGS * 64u + S.T.l], S.landings_add);
   if (S.dirty & D_LAND) sti(S.T, OUZ_I_LAND_FLAG, S.land_flag);
-  if (S.dirty & D_DR) { st(S.T, OUZ_F_DR, S.dr_m); st(S.T, OUZ_F_DR + 1, S.dr_i); st(S.T, OUZ_F_DR + 2, S.dr_t); }
+  if (S.dirty & D_DR) {
+    st(S.T, OUZ_F_DR, S.dr_m); st(S.T, OUZ_F_DR + 1, S.dr_i); st(S.T, OUZ_F_DR + 2, S.dr_t);
+    sti(S.T, OUZ_I_RAND_STEP, S.rand_step);
+  }
   if constexpr (TGT == TGT_GOAL) st3(S.T, OUZ_F_TARGET, S.target);
   if constexpr (CTRL == CTRL_RL) {
 #pragma unroll
@@ -681,11 +723,27 @@ OUZ_DEV void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid,
     if (S.land_flag < 0) S.land_flag = ldi(S.T, OUZ_I_LAND_FLAG);   // landing counter (ekf_lee_landed.py:323-331)
     if (S.land_flag) { S.landings_add += S.land_flag; S.land_flag = 0; S.dirty |= D_LAND; }
     if (tp.dr) {
-      U4 d = draw(a.seed, gid, sc.step, RNG_DR);
-      S.dr_m = uniform_f32(d.x, c.dr_lo, c.dr_hi);
-      S.dr_i = uniform_f32(d.y, c.dr_lo, c.dr_hi);
-      S.dr_t = uniform_f32(d.z, c.dr_lo, c.dr_hi);
-      S.dirty |= D_DR;
+      // VecTask.apply_randomizations at reset (vec_task.py:547-563): the envs in the reset buffer whose
+      // randomize_buf = step - OUZ_I_RAND_STEP >= frequency, and every env on its first randomization.  With
+      // frequency <= 1 and no setup_only parameter every reset is due (an env resets at most once per step), so
+      // the last step is read only otherwise.
+      const PhysDr& pd = a.pdr;
+      const int32_t last = pd.need_last ? ldi(S.T, OUZ_I_RAND_STEP) : -1;
+      const bool first = last < 0;
+      if (first || (int64_t)sc.step - (int64_t)last >= (int64_t)pd.p.frequency) {
+        const U4 d = draw(a.seed, gid, sc.step, RNG_DR);
+        U4 e{0u, 0u, 0u, 0u};
+        if (pd.gauss) e = draw(cold_seed(a.seed), gid, sc.step, RNG_DR, 1u);
+        const ouz_dr_param& pm = pd.p.param[OUZ_DRP_MASS];
+        const ouz_dr_param& pi = pd.p.param[OUZ_DRP_INERTIA];
+        const ouz_dr_param& pt = pd.p.param[OUZ_DRP_MOTOR_CONSTANT];
+        if (pm.distribution && (first || !pm.setup_only)) S.dr_m = dr_scale(pm, dr_sample(pm, d.x, e.x, sc.step), c.mass);
+        if (pi.distribution && (first || !pi.setup_only)) S.dr_i = dr_scale(pi, dr_sample(pi, d.y, e.y, sc.step), c.ixx);
+        if (pt.distribution && (first || !pt.setup_only))
+          S.dr_t = dr_scale(pt, dr_sample(pt, d.z, e.z, sc.step), kMotorConstant);
+        S.rand_step = (int32_t)sc.step;
+        S.dirty |= D_DR;
+      }
     }
     if constexpr (CTRL == CTRL_RL) {
       if (tp.fault) {
@@ -724,6 +782,10 @@ OUZ_DEV void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid,
       eff[k] = (on && S.frot == k) ? th * S.eta : th;
       if (rst) { th = 0.0f; eff[k] = 0.0f; }                        // thrusts/forces[reset] = 0
       S.thrust[k] = th;
+    }
+    if (tp.dr) {   // the rotors' motorConstant scale (ouz_dr_physical OUZ_DRP_MOTOR_CONSTANT)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) eff[k] *= S.dr_t;
     }
     float tot = 0.0f, tx = 0.0f, ty = 0.0f, tz = 0.0f;
 #pragma unroll
@@ -883,7 +945,9 @@ OUZ_DEV void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid,
   OUZ_STAMP(3, false);
   // ---- physics: gym.simulate -> lumped rigid body, c.substeps sub-steps ----
   {
-    const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * S.dr_i);
+    // additive inertia DR adds the same sample to each diagonal entry: the zz scale follows from the xx scale
+    const float dr_iz = a.pdr.inertia_add ? 1.0f + (S.dr_i - 1.0f) * (c.ixx * c.inv_izz) : S.dr_i;
+    const V3 I = v3(c.ixx * S.dr_i, c.iyy * S.dr_i, c.izz * dr_iz);
     const float inv_m = tp.dr ? 1.0f / (c.mass * S.dr_m) : c.inv_mass;
     const V3 inv_I = tp.dr ? v3(1.0f / I.x, 1.0f / I.y, 1.0f / I.z) : v3(c.inv_ixx, c.inv_iyy, c.inv_izz);
     if constexpr (TGT == TGT_TRAJ && !SPW) platform_step<CTRL, TGT>(a, sc, gid, S);
@@ -952,6 +1016,69 @@ inline const char* config_error(const ouz_config* cfg) {
   return nullptr;
 }
 
+// The tasks an env object of task cfg_task steps (the mixed curriculum: its three).
+inline bool task_used(int cfg_task, int t) {
+  return cfg_task == OUZ_TASK_MIXED ? (t == OUZ_TASK_LEE_LANDED || t == OUZ_TASK_TRACKING || t == OUZ_TASK_FAULT)
+                                    : t == cfg_task;
+}
+
+// nullptr if the physical DR parameters are valid, else what is wrong with them
+inline const char* dr_physical_error(const ouz_dr_physical* p) {
+  if (p->frequency < 0) return "frequency must be >= 0";
+  for (int k = 0; k < OUZ_DRP_COUNT; ++k) {
+    const ouz_dr_param& q = p->param[k];
+    if (q.distribution < 0 || q.distribution > 3 || q.operation < 0 || q.operation > 1 || q.schedule < 0 ||
+        q.schedule > 2)
+      return "bad distribution / operation / schedule";
+    if (q.distribution == 0) continue;
+    if (q.schedule != 0 && q.schedule_steps <= 0) return "a schedule needs schedule_steps > 0";
+    if (q.distribution == 3 && !(q.range[0] > 0.0f && q.range[1] > 0.0f)) return "a loguniform range must be positive";
+  }
+  return nullptr;
+}
+
+// The step's view of physical DR parameters (PhysDr).
+inline PhysDr derive_phys_dr(const ouz_dr_physical& p) {
+  PhysDr d;
+  memset(&d, 0, sizeof(d));
+  d.p = p;
+  bool setup = false;
+  for (int k = 0; k < OUZ_DRP_COUNT; ++k) {
+    if (!p.param[k].distribution) continue;
+    setup |= p.param[k].setup_only != 0;
+    d.gauss |= p.param[k].distribution == 1 ? 1 : 0;
+  }
+  d.need_last = (p.frequency > 1 || setup) ? 1 : 0;
+  d.inertia_add = (p.param[OUZ_DRP_INERTIA].distribution && p.param[OUZ_DRP_INERTIA].operation == 0) ? 1 : 0;
+  return d;
+}
+
+// ouz_set_dr_physical: the parameters for every task of the env object (p == nullptr or nothing enabled: off).
+inline void set_phys_dr(StepArgs& a, int cfg_task, const ouz_dr_physical* p) {
+  bool on = false;
+  if (p)
+    for (int k = 0; k < OUZ_DRP_COUNT; ++k) on |= p->param[k].distribution != 0;
+  if (on) a.pdr = derive_phys_dr(*p);
+  else memset(&a.pdr, 0, sizeof(a.pdr));
+  for (int t = 0; t < OUZ_NUM_TASKS; ++t)
+    if (task_used(cfg_task, t)) a.tp[tp_slot(t)].dr = on ? 1 : 0;
+}
+
+// The task default (QuadTracking; BASELINE.json config C): mass, inertia and motor-constant scaling ~ U(dr_lo, dr_hi)
+// at every reset, as a dr_params entry {range: [dr_lo, dr_hi], operation: scaling, distribution: uniform}.
+inline ouz_dr_physical default_phys_dr(const ouz_config* cfg) {
+  ouz_dr_physical p;
+  memset(&p, 0, sizeof(p));
+  p.frequency = 1;
+  for (int k = 0; k < OUZ_DRP_COUNT; ++k) {
+    p.param[k].distribution = 2;
+    p.param[k].operation = 1;
+    p.param[k].range[0] = cfg->dr_lo;
+    p.param[k].range[1] = cfg->dr_hi;
+  }
+  return p;
+}
+
 // StepArgs from a (valid) configuration: sizes, slot layout, ids, seed, body constants, task parameters.  The
 // buffer pointers, the waypoint table and the device-only kernel-form knobs are the caller's.
 inline void fill_step_args(const ouz_config* cfg, StepArgs& a) {
@@ -981,12 +1108,11 @@ inline void fill_step_args(const ouz_config* cfg, StepArgs& a) {
                   cfg->dr_lo, cfg->dr_hi, cfg->fault_eta_hi, (float)(4.0 * 3.14159265358979323846),
                   cfg->substeps, cfg->convergence_time, (float)mass, (float)ixx, (float)ixx, (float)izz,
                   1.0f / (float)mass, 1.0f / (float)ixx, 1.0f / (float)ixx, 1.0f / (float)izz};
+  bool preset_dr = false;
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
-    const bool used = cfg->task == OUZ_TASK_MIXED
-                          ? (t == OUZ_TASK_LEE_LANDED || t == OUZ_TASK_TRACKING || t == OUZ_TASK_FAULT)
-                          : t == cfg->task;
-    if (!used) continue;
+    if (!task_used(cfg->task, t)) continue;
     TaskParams tp = task_preset(t);
+    preset_dr |= tp.dr != 0;
     if (cfg->pomdp >= 0) tp.pomdp = cfg->pomdp;
     if (cfg->pomdp_prob >= 0.0f) tp.pomdp_prob = cfg->pomdp_prob;
     if (cfg->max_episode_length > 0) tp.max_ep = cfg->max_episode_length;
@@ -995,6 +1121,7 @@ inline void fill_step_args(const ouz_config* cfg, StepArgs& a) {
     tp.noise_hi = (float)(1.0 + prob);
     a.tp[tp_slot(t)] = tp;
   }
+  if (preset_dr) a.pdr = derive_phys_dr(default_phys_dr(cfg));   // the DR tasks' flags stay their presets'
 }
 
 // Waypoint tables of landing.py:108-112 (lemniscate(a=4,100), circle(r=2,100), square(4,8)),
@@ -1021,9 +1148,7 @@ inline void build_waypoints(float2* tab) {
 inline uint32_t flicker_mask(const StepArgs& a, int cfg_task, uint32_t step) {
   uint32_t m = 0;
   for (int t = 0; t < OUZ_NUM_TASKS; ++t) {
-    if (cfg_task != OUZ_TASK_MIXED ? t != cfg_task
-                                   : !(t == OUZ_TASK_LEE_LANDED || t == OUZ_TASK_TRACKING || t == OUZ_TASK_FAULT))
-      continue;
+    if (!task_used(cfg_task, t)) continue;
     const TaskParams& tp = a.tp[tp_slot(t)];
     if (tp.pomdp != OUZ_POMDP_FLICKER && tp.pomdp != OUZ_POMDP_FLICKER_NOISE) continue;
     const float p = tp.pomdp == OUZ_POMDP_FLICKER ? tp.pomdp_prob : 0.1f;

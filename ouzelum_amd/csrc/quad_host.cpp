@@ -97,6 +97,7 @@ inline void host_init_slot(const StepArgs& a, int cfg_task, int s) {
   for (int k = 0; k < 4; ++k) st(a, OUZ_F_EKF_P + s4(k, k), s, 1.0f);       // ahrs_ekf.py:997
   for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_P + s9(k, k), s, kPvP0);        // PVFilter.py:12
   st(a, OUZ_F_DR, s, 1.0f); st(a, OUZ_F_DR + 1, s, 1.0f); st(a, OUZ_F_DR + 2, s, 1.0f);
+  sti(a, OUZ_I_RAND_STEP, s, -1);        // never randomized: the first reset is due (vec_task.py:555-557)
   st(a, OUZ_F_FAULT_ETA, s, 1.0f);
   if (tp.target_mode == TGT_TRAJ) {      // landing.py:209-213
     U4 r = draw(a.seed, gid, INIT_STEP, RNG_TRAJ);
@@ -254,10 +255,22 @@ int ouz_host_set_trace(ouz_host_env* env, float* trace, uint32_t* resets, int32_
 
 int ouz_host_set_dr_noise(ouz_host_env* env, int32_t target, const ouz_dr_noise* dr) {
   if (!env || (target != 0 && target != 1)) return host_fail(OUZ_ERR_INVALID, "ouz_host_set_dr_noise: bad target");
+  if (dr && (dr->distribution < 0 || dr->distribution > 2 || dr->operation < 0 || dr->operation > 1 ||
+             dr->schedule < 0 || dr->schedule > 2 || (dr->schedule && dr->schedule_steps <= 0) || dr->frequency < 0))
+    return host_fail(OUZ_ERR_INVALID, "ouz_host_set_dr_noise: bad distribution / operation / schedule / frequency");
   if (dr) env->drn[target] = *dr;
   else memset(&env->drn[target], 0, sizeof(ouz_dr_noise));
   const bool on = env->drn[target].distribution != 0;
   env->a.drn_mask = on ? (env->a.drn_mask | (1 << target)) : (env->a.drn_mask & ~(1 << target));
+  return OUZ_OK;
+}
+
+int ouz_host_set_dr_physical(ouz_host_env* env, const ouz_dr_physical* dr) {
+  if (!env) return host_fail(OUZ_ERR_INVALID, "ouz_host_set_dr_physical: null env");
+  if (dr)
+    if (const char* bad = dr_physical_error(dr))
+      return host_fail(OUZ_ERR_INVALID, std::string("ouz_host_set_dr_physical: ") + bad);
+  set_phys_dr(env->a, env->cfg.task, dr);
   return OUZ_OK;
 }
 

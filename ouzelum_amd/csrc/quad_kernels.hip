@@ -930,6 +930,7 @@ __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   st(a, OUZ_F_EKF_P + s4(2, 2), i, 1.0f); st(a, OUZ_F_EKF_P + s4(3, 3), i, 1.0f);
   for (int k = 0; k < 9; ++k) st(a, OUZ_F_PV_P + s9(k, k), i, kPvP0);        // PVFilter.py:12
   st(a, OUZ_F_DR, i, 1.0f); st(a, OUZ_F_DR + 1, i, 1.0f); st(a, OUZ_F_DR + 2, i, 1.0f);
+  sti(a, OUZ_I_RAND_STEP, i, -1);        // never randomized: the first reset is due (vec_task.py:555-557)
   st(a, OUZ_F_FAULT_ETA, i, 1.0f);
   if (tp.target_mode == TGT_TRAJ) {      // landing.py:209-213
     U4 r = draw(a.seed, gid, INIT_STEP, RNG_TRAJ);
@@ -1212,7 +1213,8 @@ using namespace ouz;
 static_assert(sizeof(ouz_config) == 88, "ctypes OuzConfig mirror (ouzelum_amd/_lib.py)");
 static_assert(sizeof(ouz_buffers) == 48, "ctypes OuzBuffers mirror");
 static_assert(sizeof(ouz_task_info) == 32, "ctypes OuzTaskInfo mirror");
-static_assert(sizeof(ouz_dr_noise) == 32, "ctypes OuzDrNoise mirror");
+static_assert(sizeof(ouz_dr_noise) == 40, "ctypes OuzDrNoise mirror");
+static_assert(sizeof(ouz_dr_param) == 32 && sizeof(ouz_dr_physical) == 104, "ctypes OuzDrPhysical mirror");
 
 namespace {
 thread_local std::string g_err;
@@ -1778,14 +1780,22 @@ int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr) {
   ouz_dr_noise p{};
   if (dr) p = *dr;
   if (p.distribution < 0 || p.distribution > 2 || p.operation < 0 || p.operation > 1 || p.schedule < 0 ||
-      p.schedule > 2 || (p.schedule && p.schedule_steps <= 0))
-    return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad distribution / operation / schedule");
+      p.schedule > 2 || (p.schedule && p.schedule_steps <= 0) || p.frequency < 0)
+    return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad distribution / operation / schedule / frequency");
   env->drn_host[target] = p;
   int r = hip_check(hipMemcpy(env->drn_dev, env->drn_host, sizeof(env->drn_host), hipMemcpyHostToDevice),
                     "hipMemcpy(dr noise)");
   if (r) return r;
   env->args.drn = env->drn_dev;
   env->args.drn_mask = (env->drn_host[0].distribution ? 1 : 0) | (env->drn_host[1].distribution ? 2 : 0);
+  return OUZ_OK;
+}
+
+int ouz_set_dr_physical(ouz_env* env, const ouz_dr_physical* dr) {
+  if (!env) return fail(OUZ_ERR_INVALID, "ouz_set_dr_physical: null env");
+  if (dr)
+    if (const char* bad = dr_physical_error(dr)) return fail(OUZ_ERR_INVALID, std::string("ouz_set_dr_physical: ") + bad);
+  set_phys_dr(env->args, env->cfg.task, dr);   // by value in the launch arguments: read on the reset path only
   return OUZ_OK;
 }
 

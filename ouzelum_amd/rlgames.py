@@ -123,6 +123,12 @@ def get_rlgames_env_creator(seed, task_config, task_name, sim_device, rl_device,
     def create_rlgpu_env():
         kw = env_kwargs_from_task_config({**task_config, "name": task_name})
         env = QuadVecTask(sim_device=sim_device, rl_device=rl_device, seed=seed, **kw)
+        # the task YAML's domain randomisation (cfg/task/*.yaml task.randomize / randomization_params; a task that
+        # randomizes calls apply_randomizations at creation and on its resets, e.g. ant.py:125-126,246-248):
+        # applied once here, the kernel re-samples at every due reset
+        tcfg = task_config.get("task") or {}
+        if tcfg.get("randomize"):
+            env.apply_randomizations(tcfg.get("randomization_params") or {})
         if post_create_hook is not None:
             post_create_hook()
         return env

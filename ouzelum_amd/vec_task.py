@@ -55,6 +55,98 @@ def env_slots(task, n, env_id_offset=0):
     return out.astype(np.int64)
 
 
+DRONE_ACTOR = "Drone"    # the drone actor's name in every drone task (ekf_lee_landed.py:242, ouzelum.py:158)
+_DR_DIST = {"gaussian": 1, "uniform": 2, "loguniform": 3}
+_DR_OP = {"additive": 0, "scaling": 1}
+_DR_SCHED = {None: 0, "linear": 1, "constant": 2}
+_DR_PHYS_ATTRS = {("rigid_body_properties", "mass"): L.DRP_MASS,
+                  ("rigid_body_properties", "inertia"): L.DRP_INERTIA,
+                  ("motor_properties", "motor_constant"): L.DRP_MOTOR_CONSTANT}
+
+
+def _dr_entry(p, what, dists):
+    dist = p.get("distribution")
+    if dist not in dists:
+        raise ValueError(f"{what}: distribution {dist!r} not in {sorted(dists)}")
+    if p.get("operation") not in _DR_OP:
+        raise ValueError(f"{what}: operation {p.get('operation')!r} not in {sorted(_DR_OP)}")
+    sched = p.get("schedule")       # dr_utils.py:77-78: schedule_steps only read with a schedule
+    if sched not in _DR_SCHED:
+        raise ValueError(f"{what}: schedule {sched!r} not in ['linear', 'constant']")
+    lo, hi = (float(v) for v in p["range"])
+    return {"distribution": dists[dist], "operation": _DR_OP[p["operation"]], "range": (lo, hi),
+            "schedule": _DR_SCHED[sched], "schedule_steps": int(p["schedule_steps"]) if sched else 0}
+
+
+def parse_dr_params(dr_params):
+    """The reference's dr_params (cfg/task/*.yaml ``randomization_params``; vec_task.py:538-768) as the build's
+    integer form: ``({"observations": noise | None, "actions": noise | None}, physical | None)``, where a noise
+    entry is the ouz_dr_noise fields and ``physical`` is ``{"frequency", "params": [mass, inertia,
+    motor_constant]}`` of ouz_dr_param fields (distribution 0: not randomized), or None without ``actor_params``
+    (the task default stays).  Raises NotImplementedError for what the build does not simulate."""
+    if "sim_params" in dr_params:
+        raise NotImplementedError("sim_params randomization (gravity, PhysX solver parameters) is not implemented: "
+                                  "the build's integrator has fixed gravity and no PhysX solver (DESIGN.md §3)")
+    freq = int(dr_params.get("frequency", 1))   # vec_task.py:548
+    if freq < 0:
+        raise ValueError("frequency must be >= 0")
+    noise = {}
+    for key in ("observations", "actions"):
+        p = dr_params.get(key)
+        if not p:
+            noise[key] = None
+            continue
+        e = _dr_entry(p, key, {"gaussian": 1, "uniform": 2})
+        lc, hc = (float(v) for v in p.get("range_correlated", [0.0, 0.0]))
+        noise[key] = {**e, "range_correlated": (lc, hc), "frequency": freq}
+    if "actor_params" not in dr_params:
+        return noise, None
+    params = [{"distribution": 0, "operation": 0, "range": (0.0, 0.0), "schedule": 0, "schedule_steps": 0,
+               "setup_only": 0} for _ in range(L.DRP_COUNT)]
+    for actor, props in (dr_params["actor_params"] or {}).items():
+        if actor != DRONE_ACTOR:
+            raise NotImplementedError(f"actor {actor!r}: only the drone ({DRONE_ACTOR!r}) is simulated physics here "
+                                      "(the husky platform is kinematic, the marker visual)")
+        for prop, attrs in (props or {}).items():
+            if prop == "color":       # a visual property (vec_task.py:695-701): no renderer here
+                continue
+            if prop == "scale":
+                raise NotImplementedError("actor scale randomization is not implemented (the x500 geometry is fixed)")
+            for attr, p in (attrs or {}).items():
+                k = _DR_PHYS_ATTRS.get((prop, attr))
+                if k is None:
+                    raise NotImplementedError(f"{DRONE_ACTOR}.{prop}.{attr}: not a randomizable parameter of the lumped "
+                                              f"x500 body; one of {sorted('.'.join(x) for x in _DR_PHYS_ATTRS)}")
+                if p.get("num_buckets", 0):
+                    raise NotImplementedError("num_buckets (PhysX material buckets, dr_utils.py:135-145)")
+                e = _dr_entry(p, f"{DRONE_ACTOR}.{prop}.{attr}", _DR_DIST)
+                if e["distribution"] == 3 and not (e["range"][0] > 0 and e["range"][1] > 0):
+                    raise ValueError(f"{DRONE_ACTOR}.{prop}.{attr}: a loguniform range must be positive")
+                params[k] = {**e, "setup_only": 1 if p.get("setup_only", False) else 0}
+    return noise, {"frequency": freq, "params": params}
+
+
+def _dr_noise_struct(p):
+    s = L.OuzDrNoise()
+    if p:
+        s.distribution, s.operation = p["distribution"], p["operation"]
+        s.range[0], s.range[1] = p["range"]
+        s.range_correlated[0], s.range_correlated[1] = p["range_correlated"]
+        s.schedule, s.schedule_steps, s.frequency = p["schedule"], p["schedule_steps"], p["frequency"]
+    return s
+
+
+def _dr_physical_struct(phys):
+    s = L.OuzDrPhysical()
+    s.frequency = phys["frequency"]
+    for k, p in enumerate(phys["params"]):
+        q = s.param[k]
+        q.distribution, q.operation = p["distribution"], p["operation"]
+        q.range[0], q.range[1] = p["range"]
+        q.schedule, q.schedule_steps, q.setup_only = p["schedule"], p["schedule_steps"], p["setup_only"]
+    return s
+
+
 class QuadVecTask:
     """Vectorised x500 quadrotor env (one HIP kernel per step)."""
 
@@ -350,37 +442,35 @@ class QuadVecTask:
             self.check_health()
         return buf
 
-    _DRN_DIST = {"gaussian": 1, "uniform": 2}
-    _DRN_OP = {"additive": 0, "scaling": 1}
-    _DRN_SCHED = {None: 0, "linear": 1, "constant": 2}
-
     def apply_randomizations(self, dr_params):
-        """The non-physical part of VecTask.apply_randomizations (vec_task.py:576-646): the
-        "observations" / "actions" noise lambdas, evaluated inside the step kernel with the
-        counter RNG.  Physical entries (sim_params, actor_params) are not implemented: the drone
-        tasks disable them (EKFLeeLanded.yaml:48-49); mass / inertia / thrust DR is QuadTracking's."""
-        unknown = set(dr_params) - {"observations", "actions", "frequency"}
-        if unknown:
-            raise NotImplementedError(f"randomization entries {sorted(unknown)} are not implemented on the HIP path")
-        for target, key in ((0, "observations"), (1, "actions")):
-            if self._host:
-                L.host_check(L.host_lib().ouz_host_set_dr_noise(self._env, target, self._dr_struct(dr_params.get(key))),
-                             "ouz_host_set_dr_noise")
-                continue
-            L.check(L.lib.ouz_set_dr_noise(self._env, target, self._dr_struct(dr_params.get(key))),
-                    "ouz_set_dr_noise")
+        """VecTask.apply_randomizations (vec_task.py:538-768) for this env's physics, evaluated inside the step
+        kernel with the counter RNG (``parse_dr_params`` maps the reference's dr_params schema):
 
-    def _dr_struct(self, p):
-        s = L.OuzDrNoise()
-        if not p:
-            return s
-        s.distribution = self._DRN_DIST[p["distribution"]]
-        s.operation = self._DRN_OP[p["operation"]]
-        s.range[0], s.range[1] = p["range"]
-        s.range_correlated[0], s.range_correlated[1] = p.get("range_correlated", [0.0, 0.0])
-        s.schedule = self._DRN_SCHED[p.get("schedule")]
-        s.schedule_steps = int(p.get("schedule_steps", 0))
-        return s
+        * ``frequency`` (default 1);
+        * ``observations`` / ``actions``: the noise lambdas (:576-646), re-derived every ``frequency`` steps;
+        * ``actor_params.Drone`` (the drone actor, ekf_lee_landed.py:242): ``rigid_body_properties.mass`` /
+          ``.inertia`` and ``motor_properties.motor_constant`` (the rotors' motorConstant, model.sdf:523), each
+          ``{range, operation, distribution (uniform / loguniform / gaussian), schedule, schedule_steps,
+          setup_only}``, sampled at the lazy reset of every env whose randomize_buf >= frequency (:547-563).  An
+          ``actor_params`` entry replaces the task's default physical DR (QuadTracking: mass / inertia / motor
+          constant scaling ~ U(0.9, 1.1)); without one the default stays.
+        What this build does not simulate raises ``NotImplementedError``: ``sim_params`` (gravity, PhysX solver
+        parameters), other actors (the husky is kinematic, the marker visual), ``scale``, ``num_buckets``
+        (PhysX material buckets), other properties.  ``color`` is visual only and ignored."""
+        noise, phys = parse_dr_params(dr_params)
+        for target, key in ((0, "observations"), (1, "actions")):
+            st = _dr_noise_struct(noise[key])
+            if self._host:
+                L.host_check(L.host_lib().ouz_host_set_dr_noise(self._env, target, st), "ouz_host_set_dr_noise")
+            else:
+                L.check(L.lib.ouz_set_dr_noise(self._env, target, st), "ouz_set_dr_noise")
+        if phys is None:
+            return
+        st = _dr_physical_struct(phys)
+        if self._host:
+            L.host_check(L.host_lib().ouz_host_set_dr_physical(self._env, st), "ouz_host_set_dr_physical")
+        else:
+            L.check(L.lib.ouz_set_dr_physical(self._env, st), "ouz_set_dr_physical")
 
     def enable_trace(self, env_index=0, capacity=4096):
         """Record (p, target, v) of one env and the number of envs reset at every step, written by

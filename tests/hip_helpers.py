@@ -69,6 +69,7 @@ def gpu_to_oracle(env, oenv):
     oenv.fault_onset = iv[L.I_FAULT_ONSET].copy()
     oenv.land_flag = iv[L.I_LAND_FLAG].copy()
     oenv.landings = iv[L.I_LANDINGS].copy()
+    oenv.rand_step = iv[L.I_RAND_STEP].copy()
     oenv.reset_buf = env.reset_buf.cpu().numpy().astype(np.int64)
     oenv.sim_step = env.sim_step_count
 
@@ -83,7 +84,8 @@ def gpu_snapshot(env):
         "target": env.target_root_positions.cpu().numpy().astype(np.float64), "thrust": f[L.F_THRUST:L.F_THRUST + 4].T,
         "ekf_q": f[L.F_EKF_Q:L.F_EKF_Q + 4].T, "pv_x": f[L.F_PV_X:L.F_PV_X + 9].T,
         "waypoint": f[L.F_WAYPOINT:L.F_WAYPOINT + 3].T, "plat": f[L.F_PLAT:L.F_PLAT + 2].T,
-        "progress": iv[L.I_PROGRESS], "land_flag": iv[L.I_LAND_FLAG],
+        "progress": iv[L.I_PROGRESS], "land_flag": iv[L.I_LAND_FLAG], "dr": f[L.F_DR:L.F_DR + 3].T,
+        "rand_step": iv[L.I_RAND_STEP],
         "obs": env.obs_buf.cpu().numpy().astype(np.float64), "rew": env.rew_buf.cpu().numpy().astype(np.float64),
         "reset": env.reset_buf.cpu().numpy(), "timeouts": env.timeout_buf.cpu().numpy(),
     }

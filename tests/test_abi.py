@@ -78,7 +78,34 @@ def test_struct_layout(L):
     # must equal the static_asserts in quad_kernels.hip
     assert ctypes.sizeof(L.OuzConfig) == 88
     assert ctypes.sizeof(L.OuzBuffers) == 48
-    assert ctypes.sizeof(L.OuzTaskInfo) == 32 and ctypes.sizeof(L.OuzDrNoise) == 32
+    assert ctypes.sizeof(L.OuzTaskInfo) == 32 and ctypes.sizeof(L.OuzDrNoise) == 40
+    assert ctypes.sizeof(L.OuzDrParam) == 32 and ctypes.sizeof(L.OuzDrPhysical) == 104
+
+
+def test_dr_physical_validation_without_gpu(L):
+    """ouz_set_dr_physical / ouz_host_set_dr_physical refuse bad parameters before touching the env."""
+    p = L.OuzDrPhysical()
+    p.frequency = -1
+    assert L.lib.ouz_set_dr_physical(None, p) == -1
+    cfg = L.OuzConfig()
+    L.lib.ouz_default_config(cfg)
+    H = L.host_lib()
+    h = ctypes.c_void_p()
+    assert H.ouz_host_create(cfg, h) == 0
+    try:
+        assert H.ouz_host_set_dr_physical(h, p) == -1 and b"frequency" in H.ouz_host_last_error()
+        p.frequency = 1
+        p.param[0].distribution = 3
+        p.param[0].range[0], p.param[0].range[1] = 0.0, 1.0
+        assert H.ouz_host_set_dr_physical(h, p) == -1 and b"loguniform" in H.ouz_host_last_error()
+        p.param[0].range[0] = 0.5
+        p.param[0].schedule = 1
+        assert H.ouz_host_set_dr_physical(h, p) == -1 and b"schedule_steps" in H.ouz_host_last_error()
+        p.param[0].schedule_steps = 10
+        assert H.ouz_host_set_dr_physical(h, p) == 0
+        assert H.ouz_host_set_dr_physical(h, None) == 0
+    finally:
+        H.ouz_host_destroy(h)
 
 
 def test_argument_validation_without_gpu(L):

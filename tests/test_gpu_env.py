@@ -502,30 +502,30 @@ def test_trace_trajectory_csv_and_metrics(ouz, tmp_path):
     np.testing.assert_allclose(ra, rb, rtol=1e-5, atol=1e-5)
 
 
-def _drn_oracle(p):
-    if p is None:
-        return None
-    return {"distribution": Q.DRN_DIST[p["distribution"]], "operation": Q.DRN_OP[p["operation"]],
-            "range": p["range"], "range_correlated": p.get("range_correlated", [0.0, 0.0]),
-            "schedule": Q.DRN_SCHED[p.get("schedule")], "schedule_steps": p.get("schedule_steps", 0)}
-
-
-@pytest.mark.parametrize("obs_p,act_p", [
+@pytest.mark.parametrize("obs_p,act_p,freq", [
     ({"distribution": "gaussian", "operation": "additive", "range": [0.0, 0.05],
       "range_correlated": [0.0, 0.01], "schedule": "linear", "schedule_steps": 20},
-     {"distribution": "uniform", "operation": "scaling", "range": [0.8, 1.2]}),
+     {"distribution": "uniform", "operation": "scaling", "range": [0.8, 1.2]}, None),
     ({"distribution": "uniform", "operation": "additive", "range": [-0.1, 0.1], "schedule": "constant",
       "schedule_steps": 5},
-     {"distribution": "gaussian", "operation": "scaling", "range": [1.0, 0.2], "range_correlated": [0.0, 0.1]}),
+     {"distribution": "gaussian", "operation": "scaling", "range": [1.0, 0.2], "range_correlated": [0.0, 0.1]}, None),
+    # the parameters (schedule at the epoch, correlated draw) re-derived every 7 steps (vec_task.py:559,577)
+    ({"distribution": "gaussian", "operation": "additive", "range": [0.0, 0.05],
+      "range_correlated": [0.02, 0.03], "schedule": "linear", "schedule_steps": 20},
+     {"distribution": "uniform", "operation": "additive", "range": [-0.1, 0.1],
+      "range_correlated": [-0.2, 0.2]}, 7),
 ])
-def test_vectask_dr_noise_parity(ouz, obs_p, act_p):
+def test_vectask_dr_noise_parity(ouz, obs_p, act_p, freq):
     """VecTask.apply_randomizations' observation / action noise lambdas (vec_task.py:576-646) in the
     step kernel vs the oracle, step by step from identical states (Ouzelum: actions drive thrust)."""
+    from ouzelum_amd.vec_task import parse_dr_params
     n = 256
+    dr = {"observations": obs_p, "actions": act_p, **({"frequency": freq} if freq else {})}
     env = ouz.make(seed=8, task="Ouzelum", num_envs=n, sim_device="cuda:0")
-    env.apply_randomizations({"observations": obs_p, "actions": act_p})
-    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_OUZELUM, num_envs=n, seed=8, dr_obs=_drn_oracle(obs_p),
-                                dr_act=_drn_oracle(act_p)))
+    env.apply_randomizations(dr)
+    noise, _ = parse_dr_params(dr)
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_OUZELUM, num_envs=n, seed=8, dr_obs=noise["observations"],
+                                dr_act=noise["actions"]))
     rs = np.random.RandomState(2)
     for k in range(30):
         a = actions_for(rs, n)

@@ -63,3 +63,27 @@ def test_registration_and_env_info_shape():
     assert made == [1]
     assert e.get_env_info() == {"action_space": "A", "observation_space": "O"}
     assert e.get_number_of_agents() == 1 and e.reset_done() == "rd"
+
+
+def test_creator_applies_the_yaml_randomization_params():
+    """task.randomize / task.randomization_params of the task YAML (the reference's DR switch) reach
+    apply_randomizations through the creator; the schema is the reference's (vec_task.py:538-768)."""
+    from ouzelum_amd import _lib as L
+    cfg = R.resolve_task_config({**INLINE, "env": {**INLINE["env"], "numEnvs": 128}, "task": {
+        "randomize": True, "randomization_params": {"frequency": 3, "actor_params": {"Drone": {
+            "rigid_body_properties": {"mass": {"range": [0.5, 1.5], "operation": "scaling",
+                                               "distribution": "uniform"}}}}}}})
+    env = R.get_rlgames_env_creator(0, cfg, "EKFLeeLanded", "cpu", "cpu", -1, True)()
+    env.step(None)
+    m = env.frows(L.F_DR)[0]
+    assert float(m.min()) >= 0.5 and float(m.max()) <= 1.5 and float(m.std()) > 0.1
+    assert int((env.irows(L.I_RAND_STEP)[0] == 0).sum()) == 128
+    off = R.resolve_task_config({**INLINE, "env": {**INLINE["env"], "numEnvs": 128},
+                                 "task": {"randomize": False, "randomization_params": {"sim_params": {}}}})
+    env = R.get_rlgames_env_creator(0, off, "EKFLeeLanded", "cpu", "cpu", -1, True)()
+    env.step(None)
+    assert torch_all_ones(env.frows(L.F_DR, L.F_DR + 3))
+
+
+def torch_all_ones(t):
+    return bool((t == 1.0).all())
