@@ -10,9 +10,11 @@ synthetic batches staged in HBM before timing (train_vec.py:14-18 draws random
 actions; the Lee tasks ignore them, ekf_lee_landed.py:308).
 
 The timed loop runs the env the way a rollout collector does (RPO-LSTM/main.py:89-110:
-T env steps, then RecordEpisodeStatisticsTorch's returns): each 16-step rollout is
-ONE persistent launch (``ouz_rollout_stats``) that steps every env 16 times with its
-state in registers, writes every step's obs / rew / reset / time_outs into (16, N, ...)
+T env steps, then RecordEpisodeStatisticsTorch's returns): each rollout of up to 32
+steps (``--launch-steps``, the kernel's launch capacity; the env-only loop of
+train_vec.py:14-18 has no rollout length of its own, the learners' T is 16) is ONE
+persistent launch (``ouz_rollout_stats``) that steps every env K times with its
+state in registers, writes every step's obs / rew / reset / time_outs into (K, N, ...)
 rollout storage, and reduces the rollout's finished-episode statistics in the same
 launch; when N > 1 those statistics are all-reduced over RCCL (asynchronously, a
 block of rollouts per collective) -- the single collective of the path.
@@ -43,7 +45,8 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env-steps/sec (4096 envs) + achieved HBM GB/s vs roofline, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
-RING = 16                       # rollout length (RPO-LSTM rollout_steps = 16) and action-ring depth
+RING = 16                       # action-ring depth (RPO-LSTM rollout_steps = 16)
+MAX_LAUNCH_STEPS = 32           # steps one fused rollout launch holds (quad_kernels.hip kMaxRolloutChunk)
 
 # BASELINE.json configs measured on one GPU: (letter, task, envs per GPU, description)
 CONFIGS = {
@@ -89,6 +92,28 @@ def rollout_bytes_per_env_step(task, k=RING):
     return _STEP_OUT + act + (state + _STEP_OUT + 12) / k
 
 
+def evidence_launch_steps(n):
+    """Steps per fused launch of the rollout workloads the committed evidence profiles (scripts/kernel_driver.py):
+    the bench's default launch in the latency regime (the headline and the configs), the sweep's 16-step rollouts
+    (RING) at large N."""
+    return MAX_LAUNCH_STEPS if n <= LATENCY_REGIME_ENVS else RING
+
+
+def launch_sizes(steps, launch):
+    """The fused launches a ``steps``-step timed region runs: full launches of ``launch`` steps, then the rest."""
+    out = [launch] * (steps // launch)
+    if steps % launch:
+        out.append(steps % launch)
+    return out
+
+
+def region_rollout_bytes_per_env_step(task, steps, launch):
+    """Algorithmic bytes per env-step of a region of ``steps`` steps in launches of ``launch``: each launch's
+    per-launch state / statistics bytes spread over its own steps (rollout_bytes_per_env_step), step-weighted."""
+    ks = launch_sizes(steps, launch)
+    return sum(rollout_bytes_per_env_step(task, k) * k for k in ks) / sum(ks)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,13 +122,16 @@ def parse():
     ap.add_argument("--task", default="LeeLanded")
     ap.add_argument("--num-envs", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--launch-steps", type=int, default=MAX_LAUNCH_STEPS,
+                    help="steps per fused rollout launch (<= 32): the env-only loop (train_vec.py:14-18) has no "
+                         "rollout length of its own; 16 = the learners' T")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the other single-GPU BASELINE configs")
     ap.add_argument("--sweep", default="4194304,16777216")
     ap.add_argument("--cpu-seconds", type=float, default=24.0, help="total budget of the CPU baseline leg")
     ap.add_argument("--allreduce-batch", type=int, default=8,
-                    help="16-step rollouts whose return statistics share one all-reduce (N > 1)")
+                    help="rollouts whose return statistics share one all-reduce (N > 1)")
     ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="side file of the full record (every roofline entry with its traffic detail, the sweep, "
                          "the CPU table); the stdout line stays compact and names it")
@@ -266,6 +294,8 @@ def load_traffic(kernel, task, n):
         if not t:
             continue
         steps = d.get("steps_per_launch", 1)
+        if kernel == "rollout" and not streamed_rollout(task, n) and steps != evidence_launch_steps(n):
+            continue   # a summary of another launch length prices another workload
         raw = d.get("fetch_size_kb_raw")
         out = {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / (n * steps), 2),
                "read_bytes_per_env_step": round(d["read_bytes_corrected"] / (n * steps), 2),
@@ -300,6 +330,8 @@ def load_issue(kernel, task, n):
             d = json.load(fh)
         if d.get("lib_sha16") != sha:
             continue
+        if mode == "rollout" and d.get("steps_per_launch", 16) != evidence_launch_steps(n):
+            continue   # another launch length
         lat = n <= LATENCY_REGIME_ENVS
         us = d["wave_cycles"] / (NOMINAL_CLOCK_GHZ * 1e3) if lat else d["kernel_cycles"] / (d["clock_ghz"] * 1e3)
         # latency regime: one wave per SIMD, bound by that wave's instruction chain ("valu-issue"); large N: by
@@ -332,14 +364,16 @@ def step_kernel_name(task, n):
         and task in ("Ouzelum", "QuadFault", "Landing") else "quad_step_kernel"
 
 
-def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1):
-    """``us_per_step``: GPU time per env-step batch; a launch covers ``steps_per_launch`` steps.  A streamed
-    rollout is priced as what it runs: ``steps_per_launch`` step launches, with their bytes."""
+def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1, region_steps=None):
+    """``us_per_step``: GPU time per env-step batch; a launch covers ``steps_per_launch`` steps (a timed region of
+    ``region_steps`` steps: full launches and one shorter last launch, bytes step-weighted).  A streamed rollout is
+    priced as what it runs: ``steps_per_launch`` step launches, with their bytes."""
     streamed = kernel == "rollout" and streamed_rollout(task, n)
     if streamed:
         b = streamed_rollout_bytes_per_env_step(task, steps_per_launch)
     elif kernel == "rollout":
-        b = rollout_bytes_per_env_step(task, steps_per_launch)
+        b = (region_rollout_bytes_per_env_step(task, region_steps, steps_per_launch) if region_steps
+             else rollout_bytes_per_env_step(task, steps_per_launch))
     else:
         b = BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES
     achieved = b * n / (us_per_step * 1e-6) / 1e9
@@ -434,16 +468,21 @@ class TorchEvents:
 
 
 class Runner:
-    """One env driven by 16-step rollouts: fused (``ouz_rollout_stats``, the headline) or one launch per step
-    (``ouz_step_n_stats``, the VecTask.step path).  Statistics go to ``red``'s slots."""
+    """One env driven by rollouts of ``launch_steps``: fused (``ouz_rollout_stats``, the headline: one launch per
+    rollout) or one launch per step (``ouz_step_n_stats``, the VecTask.step path).  Statistics go to ``red``'s
+    slots."""
 
-    def __init__(self, task, n, dev, seed, rank, world, red):
+    def __init__(self, task, n, dev, seed, rank, world, red, launch_steps=MAX_LAUNCH_STEPS):
         off, total = rank * n, world * n
         self.env = make_env(task, n, dev, seed, off, total)
         self.ring = action_ring(n, dev, seed + rank)
-        self.storage = (torch.empty((RING, n, 13), device=dev), torch.empty((RING, n), device=dev),
-                        torch.empty((RING, n), dtype=torch.int64, device=dev),
-                        torch.empty((RING, n), dtype=torch.bool, device=dev))
+        self.launch = int(launch_steps)
+        if not 1 <= self.launch <= MAX_LAUNCH_STEPS:
+            raise ValueError(f"--launch-steps must be in [1, {MAX_LAUNCH_STEPS}]")
+        L = self.launch
+        self.storage = (torch.empty((L, n, 13), device=dev), torch.empty((L, n), device=dev),
+                        torch.empty((L, n), dtype=torch.int64, device=dev),
+                        torch.empty((L, n), dtype=torch.bool, device=dev))
         self.red = red
         self.plans = {}
         self.n_roll = 0
@@ -459,7 +498,7 @@ class Runner:
         done = 0
         red = self.red
         while done < steps:
-            k = min(RING, steps - done)
+            k = min(self.launch, steps - done)
             r = self.n_roll
             if fused:
                 self.plan(k)(red.slot_ptr(r))
@@ -473,11 +512,8 @@ class Runner:
     def prepare(self, steps):
         """Build (outside any timed region) the rollout plans a ``rollouts(steps)`` call will use: a plan is a
         validated, pre-bound C call, and building one costs tens of us of Python."""
-        done = 0
-        while done < steps:
-            k = min(RING, steps - done)
+        for k in launch_sizes(steps, self.launch):
             self.plan(k)
-            done += k
 
     def setup_timing(self, steps, fused=True):
         """Everything ``timed`` needs that is not the steps, done BEFORE the warmup so that the warmup's launches
@@ -527,14 +563,14 @@ class Runner:
         dev = self.dev
         torch.cuda.synchronize(dev)
         buf = torch.zeros(3, dtype=torch.float64, device=dev)
-        p = self.plan(RING)
+        p = self.plan(self.launch)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         spin()
         s.record()
         if fused:
             for _ in range(launches):
                 p(buf.data_ptr())
-            steps = launches * RING
+            steps = launches * self.launch
         else:
             steps = launches * 5
             self.env.rollout(self.ring, steps)
@@ -545,11 +581,12 @@ class Runner:
 
 def measure(task, n, dev, seed, rank, world, args, red, with_per_step=True):
     """Headline-style measurement of one config: fused rollouts (timed), then the per-step launch path."""
-    run = Runner(task, n, dev, seed, rank, world, red)
+    run = Runner(task, n, dev, seed, rank, world, red, args.launch_steps)
     run.setup_timing(args.steps)
     run.rollouts(max(args.warmup, 1))
     el, gpu_us = run.timed(args.steps, world)
-    out = {"value": n * world * args.steps / el, "ms_per_step": el / args.steps * 1e3, "kernel_us": gpu_us}
+    out = {"value": n * world * args.steps / el, "ms_per_step": el / args.steps * 1e3, "kernel_us": gpu_us,
+           "steps": args.steps}
     if with_per_step:
         run.setup_timing(args.steps, fused=False)
         run.rollouts(max(args.warmup, 1), fused=False)
@@ -605,7 +642,7 @@ def config_entry(letter, task, n, res, run, sweep=None):
          "unit": "env-steps/s", "ms_per_step": round(res["ms_per_step"], 5),
          # the PV filter's covariance step runs in f64, the rest of the step in f32
          "dtype": task_dtype(task),
-         "roofline": {**roofline_entry("rollout", task, n, res["kernel_us"], RING),
+         "roofline": {**roofline_entry("rollout", task, n, res["kernel_us"], run.launch, res["steps"]),
                       "kernel_us_source": "HIP events on the step stream around the timed region / steps",
                       "kernel_us_back_to_back": round(us_b2b, 3)}}
     if "per_step" in res:
@@ -816,9 +853,12 @@ def main():
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": task_dtype(args.task),
         "data": "synthetic",
         "config": {"workload": f"config {letter}: {n}-env {desc} ({args.task}), dt 0.01 x 2 sub-steps; "
-                               f"16-step rollouts, one persistent launch each (ouz_rollout_stats)",
+                               f"fused rollouts of up to {args.launch_steps} steps, one persistent launch each "
+                               "(ouz_rollout_stats: every step's obs / rew / reset / time_outs to rollout storage, "
+                               "episode statistics reduced in the launch)",
+                   "launch_steps": args.launch_steps, "launches": launch_sizes(args.steps, args.launch_steps),
                    "task": args.task, "num_envs_per_gpu": n, "global_envs": n * world,
-                   "parallelism": (f"env-sharded dp{world} (per-16-step-rollout return statistics, async "
+                   "parallelism": (f"env-sharded dp{world} (per-rollout return statistics, async "
                                    f"{'RCCL' if backend == 'nccl' else backend} all-reduce of "
                                    f"{args.allreduce_batch} rollouts' rows per collective)") if world > 1 else
                                   "dp1 (one GPU; each rollout's return statistics reduced inside its launch)",
@@ -827,15 +867,15 @@ def main():
                    "launcher": "bench.py" if os.environ.get("OUZ_BENCH_SPAWNED") else (
                        "torchrun" if world > 1 else None),
                    "rehearsal": bool(world > 1 and (backend != "nccl" or n_dev < world))},
-        "roofline": {**roofline_entry("rollout", args.task, n, res["kernel_us"], RING),
+        "roofline": {**roofline_entry("rollout", args.task, n, res["kernel_us"], run.launch, args.steps),
                      "kernel_us_source": "HIP events on the step stream around the timed region / steps "
-                                         "(16-step rollout launches, episode statistics fused)",
+                                         f"(rollout launches of up to {run.launch} steps, episode statistics fused)",
                      "kernel_us_back_to_back": round(us_b2b, 3),
                      "regime": "latency-bound: 4096 envs' state is L2/MALL-resident, see roofline_sweep"},
         "per_step_launch": {
             "value": round(ps["value"], 1), "ms_per_step": round(ps["ms_per_step"], 5),
             "note": "the same steps as one quad_step_kernel launch per VecTask.step (ouz_step_n_stats: one C "
-                    "call per 16-step rollout, episode statistics as a separate launch)",
+                    "call per rollout, episode statistics as a separate launch)",
             "roofline": {**roofline_entry("step", args.task, n, ps["kernel_us"]),
                          "kernel_us_back_to_back": round(us_b2b_step, 3)}},
     }

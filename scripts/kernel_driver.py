@@ -3,8 +3,9 @@ PMC passes: scripts/gpu_sq.sh).
 
     python scripts/kernel_driver.py --task LeeLanded --num-envs 4096 --mode rollout --launches 50
 --mode step:    one quad_step_kernel launch per step (VecTask.step path, ouz_step_n)
---mode rollout: 16-step quad_rollout_kernel launches with rollout storage and fused statistics (bench.py's
-                headline path)
+--mode rollout: quad_rollout_kernel launches with rollout storage and fused statistics (bench.py's headline
+                path), --launch-steps steps each (default bench.evidence_launch_steps: 32 in the latency regime,
+                the sweep's 16 above it)
 """
 import argparse
 import os
@@ -20,6 +21,7 @@ ap.add_argument("--num-envs", type=int, default=4096)
 ap.add_argument("--mode", choices=["step", "rollout"], default="rollout")
 ap.add_argument("--launches", type=int, default=50)
 ap.add_argument("--warmup", type=int, default=5)
+ap.add_argument("--launch-steps", type=int, default=None)
 a = ap.parse_args()
 
 import bench as B  # noqa: E402
@@ -28,17 +30,18 @@ from ouzelum_amd.distributed import ReturnAllReduce  # noqa: E402
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 red = ReturnAllReduce(dev, batch=1)
-run = B.Runner(a.task, a.num_envs, dev, 1234, 0, 1, red)
+k = a.launch_steps or B.evidence_launch_steps(a.num_envs)
+run = B.Runner(a.task, a.num_envs, dev, 1234, 0, 1, red, k)
 fused = a.mode == "rollout"
-steps_per_launch = B.RING if fused else 1
+steps_per_launch = k if fused else 1
 run.rollouts(a.warmup * steps_per_launch, fused=fused)
 torch.cuda.synchronize(dev)
 if fused:
-    p = run.plan(B.RING)
+    p = run.plan(k)
     buf = torch.zeros(3, dtype=torch.float64, device=dev)
     for _ in range(a.launches):
         p(buf.data_ptr())
 else:
     run.env.rollout(run.ring, a.launches)
 torch.cuda.synchronize(dev)
-print(f"{a.task} {a.num_envs} {a.mode}: {a.launches} launches", flush=True)
+print(f"{a.task} {a.num_envs} {a.mode}: {a.launches} launches of {steps_per_launch} steps", flush=True)

@@ -74,7 +74,11 @@ def main():
     kernel = "quad_rollout_kernel<" if mode == "rollout" and not streamed else "quad_step_kernel<"
     fetch, nf = avg_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", kernel)
     write, nw = avg_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", kernel)
-    steps = 16 if kernel == "quad_rollout_kernel<" else 1
+    steps = 1
+    if kernel == "quad_rollout_kernel<":   # kernel_driver.py's default launch length (bench.evidence_launch_steps)
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import evidence_launch_steps
+        steps = evidence_launch_steps(n)
     res = {"task": task, "num_envs": n, "kernel": kernel.rstrip("<"), "steps_per_launch": steps,
            "dispatches": [nf, nw], "fetch_size_kb_raw": fetch, "write_size_kb": write}
     try:

@@ -73,7 +73,11 @@ def main():
     clock = kcyc / (dur_us * 1e3)
     waves = c["SQ_WAVES"]
     wc = c["SQ_WAVE_CYCLES"]
-    steps = 16 if mode == "rollout" else 1
+    steps = 1
+    if mode == "rollout":   # kernel_driver.py's default launch length (bench.evidence_launch_steps)
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from bench import evidence_launch_steps
+        steps = evidence_launch_steps(n)
     f64 = sum(c2[k] or 0.0 for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                                      "SQ_INSTS_VALU_TRANS_F64"))
     res = {"task": task, "num_envs": n, "mode": mode, "kernel": kname.rstrip("<"), "steps_per_launch": steps,
