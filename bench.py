@@ -142,11 +142,11 @@ ESTIMATOR_TASKS = ("EKFLeeLanded", "QuadTracking", "QuadMixed")
 
 
 def task_dtype(task):
-    """The arithmetic types the step computes in, against the reference's: the estimator's EKF runs in f32 where
-    the reference's is numpy f64 (ahrs_ekf.py:1280-1337), its PV filter in f64 registers where the reference's
-    is torch f32 (PVFilter.py:25-110)."""
+    """The arithmetic types the step computes in, against the reference's: the estimator's EKF update and PV step
+    are evaluated in f64 registers with f32 storage -- the reference's EKF is numpy f64 (ahrs_ekf.py:1280-1337), its
+    PV filter torch f32 (PVFilter.py:25-110)."""
     if task in ESTIMATOR_TASKS:
-        return "f32; EKF f32 (reference numpy f64), PV f64 (reference torch f32)"
+        return "f32; EKF f64 (reference numpy f64), PV f64 (reference torch f32), f32 storage"
     return "f32"
 
 

@@ -279,6 +279,10 @@ uint32_t ouz_build_flags(void);
  * after ~70 ms instead of hanging the GPU, since the last reset: 0 unless the protocol is broken (its
  * results are then wrong).  reset != 0 zeroes the counter after reading it.  Synchronous. */
 int ouz_split_timeouts(uint32_t* out, int32_t reset);
+/* The same count on the env's device (switching to it for the call), read and zeroed in ONE device atomic, so a
+ * give-up that lands during the call is neither lost nor read twice.  The count is per device: it covers every
+ * env on that device (QuadVecTask.check_health raises if any of them gave up since the last read). */
+int ouz_env_split_timeouts(ouz_env* env, uint32_t* out, int32_t reset);
 /* Test-only: polls before a split-wave / output-wave wait gives up (0 restores the default, ~70 ms).  A small
  * value forces give-ups, so a test can check that they are reported (QuadVecTask.check_health raises). */
 int ouz_set_split_spin_limit(uint32_t polls);

@@ -104,6 +104,7 @@ SIGNATURES = {
     "ouz_source_id": (ctypes.c_char_p, []),
     "ouz_build_flags": (_U32, []),
     "ouz_split_timeouts": (_I, [_P, _I]),
+    "ouz_env_split_timeouts": (_I, [_P, ctypes.POINTER(ctypes.c_uint32), _I]),
     "ouz_set_split_spin_limit": (_I, [_U32]),
     "ouz_state_slots": (_I64, [_I, _I]),
     "ouz_env_slots": (_I, [_I, _I, _I64, _P]),
@@ -168,6 +169,23 @@ HOST_SIGNATURES = {
 _hostlib = None
 
 
+def _missing_host_features():
+    """The x86-64-v3 features (ouzelum_amd/build.py HOST_FLAGS) this CPU's /proc/cpuinfo does not list; [] where the
+    file cannot be read (not Linux) or on other architectures."""
+    import platform
+    if platform.machine() not in ("x86_64", "AMD64"):
+        return []
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("flags"):
+                    have = set(line.split(":", 1)[1].split())
+                    return [f for f in ("avx2", "fma", "bmi2", "movbe") if f not in have]
+    except OSError:
+        pass
+    return []
+
+
 def host_lib():
     """``libouzelum_cpu.so`` (loaded on first use: only make(sim_device="cpu") needs it)."""
     global _hostlib
@@ -175,6 +193,9 @@ def host_lib():
         if not os.path.exists(HOST_LIB_PATH):
             raise OuzelumError(f"{HOST_LIB_NAME} not found at {HOST_LIB_PATH}: build it first "
                                "(python -m ouzelum_amd.build)")
+        missing = _missing_host_features()
+        if missing:   # built with -march=x86-64-v3: it would die of SIGILL on this CPU
+            raise OuzelumError(f"{HOST_LIB_NAME} needs x86-64-v3 (AVX2 / FMA); this CPU lacks {missing}")
         try:
             h = ctypes.CDLL(HOST_LIB_PATH)
         except OSError as e:  # pragma: no cover - depends on the machine

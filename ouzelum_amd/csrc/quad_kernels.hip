@@ -576,6 +576,16 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, uint32_t w,
   }
   last = __shfl(last, 0, 64);
   if (!last) return;
+  // ISA assumption this hand-off rests on (not the HIP/C++ memory model): gfx950 relaxed agent-scope atomic
+  // stores are `global_store ... sc1` (write-through past this XCD's L2 to memory), the s_waitcnt vmcnt(0) above
+  // retires them before the ticket add issues, and relaxed agent-scope atomic loads are `global_load ... sc1`
+  // (they miss every non-coherent cache), so the last adder reads the memory the other waves' partials reached.
+  // MI355X_MICROARCH.md "Valid forms", first row.  tests/test_gpu_timed_kernels.py checks the fused statistics
+  // against ouz_episode_stats at 70 053 envs.  -DOUZ_STATS_ACQUIRE adds the agent-scope acquire the memory model
+  // would ask for (an A/B build: DESIGN.md §5.1 prices it).
+#ifdef OUZ_STATS_ACQUIRE
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
   double t[3] = {0.0, 0.0, 0.0};
   for (uint32_t j = lane; j < nw; j += 64u) {
 #pragma unroll
@@ -943,6 +953,11 @@ __global__ void init_state_kernel(StepArgs a, int task_cfg) {
   a.timeouts[e] = 0;
 }
 
+// ouz_env_split_timeouts: the device's split-wave give-up count, read (and zeroed) in one atomic.
+__global__ void split_timeouts_read_kernel(uint32_t* out, int reset) {
+  *out = reset ? atomicExch(&g_ouz_split_timeouts, 0u) : atomicAdd(&g_ouz_split_timeouts, 0u);
+}
+
 __global__ void mark_reset_kernel(int64_t* reset, const int32_t* ids, int32_t n, int32_t n_envs) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) {
@@ -1252,6 +1267,7 @@ struct ouz_env {
   uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
   double* wave_partials;     // [tiles][3] per-wave partials of the fused rollout statistics
   uint32_t* wave_ticket;     // their last-wave counter (returns to 0 after every launch)
+  uint32_t* health_word;     // ouz_env_split_timeouts' read-back word (in the wave partials' tail)
   StepArgs args;    // pre-filled launch arguments
   // ouz_rollout as one step launch per step, outputs straight into the storage rows (streamed rollout):
   // above the latency regime the fused kernel's 16 steps of state in registers cost occupancy (LeeLanded
@@ -1278,6 +1294,21 @@ int ouz_split_timeouts(uint32_t* out, int32_t reset) {
   const uint32_t zero = 0;
   return hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_ouz_split_timeouts), &zero, sizeof(uint32_t)),
                    "hipMemcpyToSymbol(split timeouts)");
+}
+
+int ouz_env_split_timeouts(ouz_env* env, uint32_t* out, int32_t reset) {
+  if (!env || !out) return fail(OUZ_ERR_INVALID, "ouz_env_split_timeouts: null pointer");
+  int prev = 0;
+  int r = hip_check(hipGetDevice(&prev), "hipGetDevice");
+  if (r) return r;
+  if (prev != env->cfg.device && (r = hip_check(hipSetDevice(env->cfg.device), "hipSetDevice"))) return r;
+  // the read and the reset in ONE device atomic: a give-up counted between them is neither lost nor read twice
+  hipLaunchKernelGGL(split_timeouts_read_kernel, dim3(1), dim3(1), 0, nullptr, env->health_word, reset ? 1 : 0);
+  r = hip_check(hipGetLastError(), "split_timeouts_read_kernel");
+  if (!r) r = hip_check(hipMemcpy(out, env->health_word, sizeof(uint32_t), hipMemcpyDeviceToHost),
+                        "hipMemcpy(split timeouts)");
+  if (prev != env->cfg.device) (void)hipSetDevice(prev);
+  return r;
 }
 
 int ouz_set_split_spin_limit(uint32_t polls) {
@@ -1383,6 +1414,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   r = hip_check(hipMalloc(&e->wave_partials, n_waves * 3 * sizeof(double) + 64), "hipMalloc(wave partials)");
   if (r) { (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   e->wave_ticket = reinterpret_cast<uint32_t*>(e->wave_partials + n_waves * 3);
+  e->health_word = e->wave_ticket + 2;
   r = hip_check(hipMemset(e->wave_ticket, 0, sizeof(uint32_t)), "hipMemset(wave ticket)");
   if (r) { (void)hipFree(e->wave_partials); (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials);
            (void)hipFree(e->wp_tab); delete e; return r; }

@@ -99,6 +99,21 @@ OUZ_HD T recip(T x) {
   return T(1) / x;
 }
 
+// 1 / sqrt(x) for x > 0.  On the device, f64: the hardware estimate refined by two Newton steps (full double
+// precision) instead of the correctly rounded sqrt sequence followed by a division.
+template <typename T>
+OUZ_HD T rsqrt_r(T x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (std::is_same_v<T, double>) {
+    double y = __builtin_amdgcn_rsq(x);
+    double h = 0.5 * x;
+    y = y * (1.5 - h * y * y);
+    return y * (1.5 - h * y * y);
+  }
+#endif
+  return T(1) / sqrt(x);
+}
+
 // ---------------------------------------------------------------------------
 // rotations
 // ---------------------------------------------------------------------------
@@ -270,33 +285,35 @@ OUZ_HD int s4(int i, int j) {  // packed index, any order
   return a * 4 - (a * (a - 1)) / 2 + (b - a);
 }
 
-// Full symmetric 4x4 inverse via Cholesky (S is SPD: P_t + 1e-7 I).
-OUZ_HD void inv_spd4(const float S[10], float Si[10]) {
-  float L[4][4] = {};
+// Full symmetric 4x4 inverse via Cholesky (S is SPD: P_t + 1e-7 I), in R.  The pivots L[j][j] are only ever used
+// through their inverses (the off-diagonal sums and Linv run over k < j), so each is one reciprocal square root.
+template <typename R>
+OUZ_HD void inv_spd4(const R S[10], R Si[10]) {
+  R L[4][4] = {};
+  R Ld[4];   // 1 / L[j][j]
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    float d = S[s4(j, j)];
+    R d = S[s4(j, j)];
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= L[j][k] * L[j][k];
-    float ljj = sqrtf(d);
-    L[j][j] = ljj;
-    float inv = 1.0f / ljj;
+    const R inv = rsqrt_r(d);
+    Ld[j] = inv;
 #pragma unroll
     for (int i = j + 1; i < 4; ++i) {
-      float s = S[s4(i, j)];
+      R s = S[s4(i, j)];
 #pragma unroll
       for (int k = 0; k < j; ++k) s -= L[i][k] * L[j][k];
       L[i][j] = s * inv;
     }
   }
   // Linv (lower)
-  float Li[4][4] = {};
+  R Li[4][4] = {};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    Li[i][i] = 1.0f / L[i][i];
+    Li[i][i] = Ld[i];
 #pragma unroll
     for (int j = 0; j < i; ++j) {
-      float s = 0.0f;
+      R s = R(0);
 #pragma unroll
       for (int k = j; k < i; ++k) s += L[i][k] * Li[k][j];
       Li[i][j] = -s * Li[i][i];
@@ -307,7 +324,7 @@ OUZ_HD void inv_spd4(const float S[10], float Si[10]) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = i; j < 4; ++j) {
-      float s = 0.0f;
+      R s = R(0);
 #pragma unroll
       for (int k = j; k < 4; ++k) s += Li[k][i] * Li[k][j];
       Si[s4(i, j)] = s;
@@ -317,79 +334,97 @@ OUZ_HD void inv_spd4(const float S[10], float Si[10]) {
 constexpr float kEkfGNoise = 0.09f;   // 0.3**2, ahrs_ekf.py:1004
 constexpr float kEkfAngR = 1e-7f;      // ahrs_ekf.py:1332
 
-// In: q (normalised prior), P. Out: q, P updated in place.
-OUZ_HD void ekf_update(EkfQ& q, float P[10], V3 g, EkfQ ang, float Dt) {
-  const float h = 0.5f * Dt;
+// The EKF update is evaluated in EkfReal and stored in f32 (q, P), like the PV step: the reference's EKF is
+// numpy float64 (ahrs_ekf.py:1280-1337).  float restores the round-4 f32 evaluation (an A/B build: -DOUZ_EKF_F32).
+#ifdef OUZ_EKF_F32
+typedef float EkfReal;
+#else
+typedef double EkfReal;
+#endif
+
+// In: q (normalised prior), P. Out: q, P updated in place.  Constants are the reference's Python floats (f64):
+// 0.5 * Dt with Dt = 1 / frequency, g_noise = 0.3 ** 2, the 1e-7 measurement noise.
+template <typename R>
+OUZ_HD void ekf_update_t(EkfQ& q, float Pf[10], V3 gf, EkfQ ang, float Dt) {
+  const R h = R(0.5) * R(Dt);
+  const R gx = gf.x, gy = gf.y, gz = gf.z;
+  const R r = sizeof(R) == 8 ? R(1e-7) : R(kEkfAngR);
+  const R gnoise = sizeof(R) == 8 ? R(0.09) : R(kEkfGNoise);
+  R P[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) P[k] = (R)Pf[k];
   // Omega(x) rows (ahrs_ekf.py:1072-1106)
-  float O[4][4] = {{0.0f, -g.x, -g.y, -g.z}, {g.x, 0.0f, g.z, -g.y}, {g.y, -g.z, 0.0f, g.x}, {g.z, g.y, -g.x, 0.0f}};
-  float qv[4] = {q.w, q.x, q.y, q.z};
-  float qt[4];
-  float F[4][4];
+  const R O[4][4] = {{R(0), -gx, -gy, -gz}, {gx, R(0), gz, -gy}, {gy, -gz, R(0), gx}, {gz, gy, -gx, R(0)}};
+  const R qv[4] = {(R)q.w, (R)q.x, (R)q.y, (R)q.z};
+  R qt[4];
+  R F[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    float s = 0.0f;
+    R s = R(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float fij = (i == j ? 1.0f : 0.0f) + h * O[i][j];   // f(): (I + 0.5 Dt Omega(g)) q
+      R fij = (i == j ? R(1) : R(0)) + h * O[i][j];   // f(): (I + 0.5 Dt Omega(g)) q
       s += fij * qv[j];
-      F[i][j] = (i == j ? 1.0f : 0.0f) + O[i][j] * h;     // dfdq: I + Omega(0.5 Dt g)
+      F[i][j] = (i == j ? R(1) : R(0)) + O[i][j] * h;  // dfdq: I + Omega(0.5 Dt g)
     }
     qt[i] = s;
   }
   // W = 0.5 Dt [ -q_v^T ; q_w I + skew(q_v) ]   (4x3), Q_t = 0.5 Dt g_noise W W^T
-  float W[4][3] = {{-q.x, -q.y, -q.z}, {q.w, -q.z, q.y}, {q.z, q.w, -q.x}, {-q.y, q.x, q.w}};
+  R W[4][3] = {{-qv[1], -qv[2], -qv[3]}, {qv[0], -qv[3], qv[2]}, {qv[3], qv[0], -qv[1]}, {-qv[2], qv[1], qv[0]}};
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) W[i][j] *= h;
   // FP (4x4 full)
-  float FP[4][4];
+  R FP[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float s = 0.0f;
+      R s = R(0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) s += F[i][k] * P[s4(k, j)];
       FP[i][j] = s;
     }
-  float Pt[10];
-  const float qs = h * kEkfGNoise;
+  R Pt[10];
+  const R qs = h * gnoise;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = i; j < 4; ++j) {
-      float s = 0.0f;
+      R s = R(0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) s += FP[i][k] * F[j][k];
-      float ww = W[i][0] * W[j][0] + W[i][1] * W[j][1] + W[i][2] * W[j][2];
+      R ww = W[i][0] * W[j][0] + W[i][1] * W[j][1] + W[i][2] * W[j][2];
       Pt[s4(i, j)] = s + qs * ww;
     }
   // S = P_t + r I ; stable identities:
   //   (I - K) P_t = r I - r^2 S^-1 ,  q_t + K v = ang - r S^-1 v
-  float S[10];
+  R S[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) S[k] = Pt[k];
-  S[s4(0, 0)] += kEkfAngR; S[s4(1, 1)] += kEkfAngR; S[s4(2, 2)] += kEkfAngR; S[s4(3, 3)] += kEkfAngR;
-  float Si[10];
-  inv_spd4(S, Si);
-  float av[4] = {ang.w, ang.x, ang.y, ang.z};
-  float vv[4] = {av[0] - qt[0], av[1] - qt[1], av[2] - qt[2], av[3] - qt[3]};
-  float qn[4];
+  S[s4(0, 0)] += r; S[s4(1, 1)] += r; S[s4(2, 2)] += r; S[s4(3, 3)] += r;
+  R Si[10];
+  inv_spd4<R>(S, Si);
+  const R av[4] = {(R)ang.w, (R)ang.x, (R)ang.y, (R)ang.z};
+  const R vv[4] = {av[0] - qt[0], av[1] - qt[1], av[2] - qt[2], av[3] - qt[3]};
+  R qn[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    float s = 0.0f;
+    R s = R(0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) s += Si[s4(i, j)] * vv[j];
-    qn[i] = av[i] - kEkfAngR * s;
+    qn[i] = av[i] - r * s;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = i; j < 4; ++j) P[s4(i, j)] = (i == j ? kEkfAngR : 0.0f) - (kEkfAngR * kEkfAngR) * Si[s4(i, j)];
-  float inv = 1.0f / sqrtf(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
-  q = EkfQ{qn[0] * inv, qn[1] * inv, qn[2] * inv, qn[3] * inv};
+    for (int j = i; j < 4; ++j) Pf[s4(i, j)] = (float)((i == j ? r : R(0)) - (r * r) * Si[s4(i, j)]);
+  const R inv = rsqrt_r(qn[0] * qn[0] + qn[1] * qn[1] + qn[2] * qn[2] + qn[3] * qn[3]);
+  q = EkfQ{(float)(qn[0] * inv), (float)(qn[1] * inv), (float)(qn[2] * inv), (float)(qn[3] * inv)};
 }
+
+OUZ_HD void ekf_update(EkfQ& q, float P[10], V3 g, EkfQ ang, float Dt) { ekf_update_t<EkfReal>(q, P, g, ang, Dt); }
 
 // ---------------------------------------------------------------------------
 // Position/velocity KF (PVFilter.py:25-110), SURVEY a13.

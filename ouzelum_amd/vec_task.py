@@ -412,7 +412,8 @@ class QuadVecTask:
         if self._host:
             return
         v = ctypes.c_uint32(0)
-        L.check(L.lib.ouz_split_timeouts(ctypes.byref(v), 1), "ouz_split_timeouts")
+        # on this env's device, read and zeroed in one atomic (the count covers every env on the device)
+        L.check(L.lib.ouz_env_split_timeouts(self._env, ctypes.byref(v), 1), "ouz_env_split_timeouts")
         if v.value:
             raise L.OuzelumError(f"{v.value} split-wave wait(s) of a fused rollout gave up (a broken LDS protocol "
                                  "or a stalled partner wave): the rollouts since the last check are wrong")

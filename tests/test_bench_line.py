@@ -92,7 +92,7 @@ def test_detail_file_written(tmp_path, full):
 def test_estimator_dtype_label_states_precision():
     assert B.task_dtype("LeeLanded") == "f32"
     lab = B.task_dtype("QuadTracking")
-    assert "EKF f32 (reference numpy f64)" in lab and "(reference torch f32)" in lab
+    assert "EKF f64 (reference numpy f64)" in lab and "PV f64 (reference torch f32)" in lab and "f32 storage" in lab
 
 
 def test_launcher_reports_failed_rank():

@@ -66,7 +66,10 @@ def test_lee_vs_reference_golden(L, golden, mode, seed):
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_ekf_sequence_vs_reference_golden(L, golden, seed):
-    """30 chained EKF.update steps per env (ahrs_ekf.py:1280-1337), f32 stable form vs f64 reference."""
+    """30 chained EKF.update steps per env (ahrs_ekf.py:1280-1337): the stable form evaluated in f64 (the
+    reference's numpy precision) with f32 storage of q and P, against the reference's f64 run.  Bounds: the f32
+    storage of a unit quaternion (6e-8) and of the O(1e-7) covariance entries; the round-4 f32 evaluation was
+    within 2e-6 (q) and 2e-6 relative (P)."""
     g = golden("ekf.npz")
     dt = float(g["dt"])
     q = g[f"s{seed}_q0"].astype(np.float32)
@@ -80,12 +83,12 @@ def test_ekf_sequence_vs_reference_golden(L, golden, seed):
         L.check(L.lib.ouz_ekf_update(qn.data_ptr(), Pd.data_ptr(), gyr.data_ptr(), ang.data_ptr(), dt, qo.data_ptr(),
                                      Po.data_ptr(), n, stream()))
         qd, Pd = qo.clone(), Po.clone()
-        # quaternion: f32 round-off on a unit vector
-        np.testing.assert_allclose(qd.cpu().numpy(), g[f"s{seed}_q"][step], atol=2e-6)
+        # quaternion: f32 storage of a unit vector (and the f32 normalisation of the prior above)
+        np.testing.assert_allclose(qd.cpu().numpy(), g[f"s{seed}_q"][step], atol=1e-7)
         # covariance entries are O(1e-7): relative to the largest entry
         Pg = g[f"s{seed}_P"][step]
         Ph = unpack_sym(Pd.cpu().numpy().astype(np.float64), 4)
-        assert np.abs(Ph - Pg).max() <= 1e-4 * np.abs(Pg).max(), step
+        assert np.abs(Ph - Pg).max() <= 5e-7 * np.abs(Pg).max(), step
 
 
 def _relerr(a, b):
