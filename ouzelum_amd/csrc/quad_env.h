@@ -10,6 +10,7 @@
 #ifdef OUZ_HOST
 #include "host_compat.h"
 #endif
+#include <cstdlib>
 #include "../../include/ouzelum.h"
 #include "quad_math.h"
 
@@ -80,8 +81,18 @@ __host__ __device__ constexpr bool class_layout_task(int task) {
 __host__ __device__ constexpr bool class_layout(int task, int n) {
   return class_layout_task(task) && n <= kLatencyRegimeEnvs;
 }
-__host__ __device__ inline int state_slots(int task, int n) {
-  if (!class_layout(task, n)) return n;
+// The trigger-class layout above the latency regime as well (OUZ_CLS_LARGE=1 in the environment at env creation
+// and for ouz_state_slots / ouz_env_slots, which must agree): there the class blocks' waves are packed onto one
+// XCD each (StepArgs.xcd_pack), so the partial output lines of a block's waves meet in that XCD's L2.
+inline bool cls_large_requested() {
+  const char* v = std::getenv("OUZ_CLS_LARGE");
+  return v && std::atoi(v) != 0;
+}
+inline bool class_layout_rt(int task, int n) {
+  return class_layout(task, n) || (class_layout_task(task) && cls_large_requested());
+}
+inline int state_slots(int task, int n) {
+  if (!class_layout_rt(task, n)) return n;
   const int blocks = (n + kClassBlock - 1) / kClassBlock;
   return (task == OUZ_TASK_MIXED ? blocks + 1 : blocks) * kClassBlock;
 }
@@ -182,6 +193,7 @@ struct StepArgs {
   int32_t quad;                // trigger-class layout: the quad-lane estimator kernels (OUZ_QUAD_LANE=1; quad_pv_ql.h)
   int32_t split;               // trigger-class layout: the split-wave estimator rollout (OUZ_SPLIT_PV; quad_pv_split.h)
   int32_t outw;                // latency-regime rollouts with an output wave (OUZ_OUT_WAVE; out_wave)
+  int32_t xcd_pack;            // class layout above the latency regime: a class block's waves on one XCD (xcd_tile)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env
@@ -1086,7 +1098,8 @@ inline void fill_step_args(const ouz_config* cfg, StepArgs& a) {
   memset(&a, 0, sizeof(a));
   a.n = cfg->num_envs;
   a.n_slots = state_slots(cfg->task, cfg->num_envs);
-  a.cls = class_layout(cfg->task, cfg->num_envs) ? (cfg->task == OUZ_TASK_MIXED ? 2 : 1) : 0;
+  a.cls = class_layout_rt(cfg->task, cfg->num_envs) ? (cfg->task == OUZ_TASK_MIXED ? 2 : 1) : 0;
+  a.xcd_pack = (a.cls && cfg->num_envs > kLatencyRegimeEnvs) ? 1 : 0;
   a.env_offset = (uint32_t)cfg->env_id_offset;
   a.n_total = (uint64_t)total;
   a.seed = cfg->seed;

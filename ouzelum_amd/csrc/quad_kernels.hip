@@ -602,6 +602,20 @@ __device__ __forceinline__ void reduce_stats(const RolloutStats& rs, uint32_t w,
   }
 }
 
+// XCD-packed class blocks (StepArgs.xcd_pack; the trigger-class layout above the latency regime): workgroup x runs
+// on XCD x % 8 (the dispatcher deals workgroups round-robin over the XCDs), and the waves of XCD c take the tiles of
+// class blocks c, c + 8, c + 16, ... in order, so the 21 waves of a block -- whose env-order outputs, 21 envs
+// apart per lane, share partial lines -- run on one XCD at about the same time and their plain stores meet in
+// that XCD's L2 instead of reaching memory as partial writes from eight L2s.  Returns this wave's tile, or -1
+// past the last block (the grid is rounded up to whole blocks per XCD).
+__device__ __forceinline__ int xcd_tile(int waves_per_wg, int n_blocks) {
+  const uint32_t x = blockIdx.x, xcd = x & 7u;
+  const uint32_t p = (x >> 3) * (uint32_t)waves_per_wg + (threadIdx.x >> 6);
+  const uint32_t b = xcd + 8u * (p / (uint32_t)kTrigClasses);
+  if (b >= (uint32_t)n_blocks) return -1;
+  return (int)__builtin_amdgcn_readfirstlane(b * (uint32_t)kTrigClasses + p % (uint32_t)kTrigClasses);
+}
+
 // The quad-lane estimator (quad_pv_ql.h) runs the trigger-class layout of the estimator tasks and the
 // QuadTracking chunks of the mixed curriculum's class layout: 64-lane blocks (the latency regime), four per
 // 64-slot tile, each wave stepping 16 envs with 4 lanes each (quad_grid_blocks on the host).
@@ -735,7 +749,13 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     if (sm) reduce_stats(*rst, blockIdx.x, gridDim.x, ls);   // every wave of the exact grid takes part
     return;
   }
-  const int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
+  int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
+  if constexpr (CLS) {
+    if (a.xcd_pack) {   // class layout above the latency regime: this wave's tile on its XCD (xcd_tile)
+      const int t = xcd_tile(step_block_for(a.n) / 64, a.n_slots / kClassBlock);
+      i = (t < 0 ? a.n_slots : t * 64) + (int)(threadIdx.x & 63u);
+    }
+  }
   const int first = i - (int)(threadIdx.x & 63);
   if (first >= (CLS ? a.n_slots : a.n)) return;   // whole wave past the end
   int e = i;                                       // env index (a.n: an idle slot)
@@ -1350,7 +1370,7 @@ int ouz_env_slots(int32_t task, int32_t num_envs, int64_t env_id_offset, int32_t
   if (task < 0 || task >= OUZ_NUM_TASKS || num_envs <= 0 || !env_slot || env_id_offset < 0 ||
       env_id_offset + num_envs > 0xFFFFFFFFll)
     return fail(OUZ_ERR_INVALID, "ouz_env_slots: bad arguments");
-  const bool cls = class_layout(task, num_envs);
+  const bool cls = class_layout_rt(task, num_envs);
   for (int32_t e = 0; e < num_envs; ++e)
     env_slot[e] = !cls ? e : (task == OUZ_TASK_MIXED ? mixed_env_slot((uint32_t)env_id_offset, e) : env_slot_of(e));
   return OUZ_OK;
@@ -1443,10 +1463,11 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     // the quad-lane estimator kernels (quad_pv_ql.h): bit-identical results, opt-in -- measured slower than the
     // one-lane kernels at 4096 envs (its LDS exchanges cost more than the f64 work they split)
     const char* ql = std::getenv("OUZ_QUAD_LANE");
-    a.quad = (a.cls && ql && std::atoi(ql) != 0) ? 1 : 0;
+    const bool lat = cfg->num_envs <= kLatencyRegimeEnvs;   // the multi-wave forms are latency-regime grids
+    a.quad = (a.cls && lat && ql && std::atoi(ql) != 0) ? 1 : 0;
     // the split-wave estimator rollout (quad_pv_split.h): bit-identical results; OUZ_SPLIT_PV=0 / 1 overrides
     const char* sp = std::getenv("OUZ_SPLIT_PV");
-    a.split = (a.cls && !a.quad && (sp ? std::atoi(sp) != 0 : kSplitDefault)) ? 1 : 0;
+    a.split = (a.cls && lat && !a.quad && (sp ? std::atoi(sp) != 0 : kSplitDefault)) ? 1 : 0;
     // the output wave while the rollout's waves stay within one per SIMD (256 tiles); OUZ_OUT_WAVE=0 / 1 overrides
     const char* ow = std::getenv("OUZ_OUT_WAVE");
     // (the mixed curriculum has the output-wave form in its class layout only)
@@ -1525,6 +1546,8 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
     }
     if (a.cls) {
       if (single) hipLaunchKernelGGL((quad_step_kernel<T, true>), g, b, 0, s, a, r.ctx[0]);
+      else if (rollout_wpe(T, a.n) > 1)
+        hipLaunchKernelGGL((quad_rollout_kernel<T, true, false, false, false, OUZ_EST_ROLLOUT_WPE>), g, b, 0, s, a, r);
       else hipLaunchKernelGGL((quad_rollout_kernel<T, true>), g, b, 0, s, a, r);
       return;
     }
@@ -1587,6 +1610,10 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
     r.ctx[k].actions = ring ? ring + (size_t)((ring_pos + k) % ring_len) * n * OUZ_NUM_ACT : nullptr;
   }
   dim3 g(grid_for(a.n_slots, blk)), b(blk);   // one lane per state slot
+  if (a.xcd_pack) {   // whole class blocks per XCD (xcd_tile)
+    const int per_xcd = (a.n_slots / kClassBlock + 7) / 8 * kTrigClasses;
+    g = dim3(8 * ((per_xcd + blk / 64 - 1) / (blk / 64)));
+  }
   const bool single = K == 1 && !storage && !stats_mode;
 #define OUZ_LAUNCH_TASK(T) launch_task<T>(single, a, r, g, b, s)
   switch (env->cfg.task) {

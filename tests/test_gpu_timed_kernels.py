@@ -254,3 +254,37 @@ def test_full_episode_through_rollout_plan(ouz, seed):
     env.check_health()
     print(f"QuadTracking seed {seed} via rollout_plan: clean envs per checkpoint {clean_counts}, worst clean |dp| "
           f"{worst_clean:.3g} |dv| {worst_clean_v:.3g}")
+
+
+@pytest.mark.parametrize("task", ["QuadTracking", "QuadMixed"])
+def test_cls_large_layout_is_bitwise_the_identity_layout(ouz, task, monkeypatch):
+    """OUZ_CLS_LARGE=1 (the trigger-class layout above 65 536 envs, class blocks packed per XCD; opt-in, DESIGN.md
+    §5.1) changes where each env's state lives and which waves take the PV fixes, not the arithmetic: rollout storage,
+    env-order state and the fused statistics equal the identity layout's bit for bit, through the per-step kernel and
+    the fused rollout."""
+    from ouzelum_amd import _lib as L
+    n = 70016 + 37
+    kw = dict(seed=27, task=task, num_envs=n, sim_device="cuda:0", track_episodes=True, convergence_time=10,
+              max_episode_length=30)
+    monkeypatch.setenv("OUZ_CLS_LARGE", "1")
+    a = ouz.make(**kw)
+    assert a._env_slot is not None and a.fstate.shape[0] * L.TILE % L.MIXED_CHUNK == 0
+    monkeypatch.delenv("OUZ_CLS_LARGE")
+    b = ouz.make(**kw)
+    assert b._env_slot is None
+    ring = (torch.rand((RING, n, 4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 2
+            - 1).contiguous()
+    for env in (a, b):
+        env.rollout(ring, 12)                           # per-step kernel launches
+    outs = []
+    for env in (a, b):
+        st = storage_for(RING, n)
+        got = torch.zeros(3, dtype=torch.float64, device="cuda")
+        env.rollout(ring, RING, fused=True, storage=st, stats_out=got)
+        outs.append((st, got))
+    torch.cuda.synchronize()
+    for x, y in zip(outs[0][0], outs[1][0]):
+        assert torch.equal(x, y)
+    assert torch.equal(outs[0][1], outs[1][1]) and float(outs[0][1][1]) > 0
+    assert torch.equal(a.frows(0, L.F_COUNT), b.frows(0, L.F_COUNT))
+    assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT))
