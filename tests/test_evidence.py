@@ -49,7 +49,7 @@ def test_issue_evidence_of_this_build(kernel, task, n):
 
 def test_committed_bench_line_is_of_this_build():
     """The driver-argument bench line committed with the evidence carries traffic and the issue view."""
-    lines = sorted(glob.glob(os.path.join(ROOT, "profiles", "r04", "bench", "bench_driver_*.jsonl")))
+    lines = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "bench", "bench_driver_*.jsonl")))
     assert lines
     with open(lines[-1]) as fh:
         d = json.loads(fh.readline())
