@@ -51,7 +51,9 @@ for it in range(a.warmup + a.iters):
         pomdps[s] = pomdp
         obs[s] = next_obs
         dones[s] = next_done
-        act, lp, _, lstm = agent.act(next_obs, lstm, next_done)
+        # alias=True: the policy graph's output buffers, as learners/train.py's loop takes them (actions[s] /
+        # logprobs[s] copy them before the next replay); alias=False adds 5 clones per step
+        act, lp, _, lstm = agent.act(next_obs, lstm, next_done, alias=True)
         actions[s] = act
         logprobs[s] = lp
         next_obs, rewards[s], next_done, info = env.step(act)
