@@ -275,7 +275,7 @@ def test_cls_large_layout_is_bitwise_the_identity_layout(ouz, task, monkeypatch)
     ring = (torch.rand((RING, n, 4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 2
             - 1).contiguous()
     for env in (a, b):
-        env.rollout(ring, 12)                           # per-step kernel launches
+        env.rollout(ring, 20)   # per-step kernel launches; the fused 16 steps then cross max_episode_length
     outs = []
     for env in (a, b):
         st = storage_for(RING, n)
