@@ -219,9 +219,11 @@ class QuadVecTask:
                 raise L.OuzelumError(f"ouz_state_slots: {L.lib.ouz_last_error().decode()}")
             self.fstate = torch.zeros((L.tiles(slots), L.F_COUNT, L.TILE), dtype=torch.float32, device=self.device)
             self.istate = torch.zeros((L.tiles(slots), L.I_COUNT, L.TILE), dtype=torch.int32, device=self.device)
-            # env -> state slot (None: slot i is env i)
-            self._env_slot = (None if slots == n else
-                              torch.from_numpy(env_slots(self.task, n, cfg.env_id_offset)).to(self.device))
+            # env -> state slot (None: slot i is env i).  Decided from the slot map itself, not from the slot
+            # count: a class layout of exactly k * 1344 envs has as many slots as envs
+            es = env_slots(self.task, n, cfg.env_id_offset)
+            self._env_slot = None if np.array_equal(es, np.arange(n)) else torch.from_numpy(es).to(self.device)
+            del es
             self.obs_buf = torch.empty((n, L.NUM_OBS), dtype=torch.float32, device=self.device)
             self.rew_buf = torch.empty(n, dtype=torch.float32, device=self.device)
             self.reset_buf = torch.empty(n, dtype=torch.int64, device=self.device)

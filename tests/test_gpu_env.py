@@ -61,12 +61,14 @@ def assert_close(name, a, b, atol, rtol):
 
 # QuadMixed assigns tasks to 1344-id chunks: shards straddling the LeeLanded | QuadTracking and the
 # QuadTracking | QuadFault chunk boundaries
-PARITY_CASES = [(t, 0) for t in TASKS if t != "QuadMixed"] + [("QuadMixed", 1244), ("QuadMixed", 2588)]
+# (task, env_id_offset, num_envs); 1344 / 2688 envs: a trigger-class layout with as many slots as envs (k class
+# blocks), still not the identity map
+PARITY_CASES = ([(t, 0, 320) for t in TASKS if t != "QuadMixed"] + [("QuadMixed", 1244, 320), ("QuadMixed", 2588, 320)]
+                + [("QuadTracking", 0, 1344), ("EKFLeeLanded", 0, 2688)])
 
 
-@pytest.mark.parametrize("task,off", PARITY_CASES)
-def test_single_step_parity(ouz, task, off):
-    n = 320
+@pytest.mark.parametrize("task,off,n", PARITY_CASES)
+def test_single_step_parity(ouz, task, off, n):
     kw = {"convergence_time": 25} if task in ("EKFLeeLanded", "QuadTracking", "QuadMixed") else {}
     if off:
         kw.update(env_id_offset=off, num_envs_total=off + n + 1000)

@@ -45,13 +45,15 @@ def assert_close(name, a, b, atol, rtol):
         raise AssertionError(f"{name}: max violation at {idx}: host={a[idx]!r} oracle={b[idx]!r}")
 
 
-PARITY_CASES = [(t, 0) for t in TASKS if t != "QuadMixed"] + [("QuadMixed", 1244)]
+# (task, env_id_offset, num_envs).  1344 / 2688 envs: a trigger-class layout with exactly as many slots as envs
+# (k class blocks), which is still not the identity map -- env-order reads must go through the slot map
+PARITY_CASES = ([(t, 0, 160) for t in TASKS if t != "QuadMixed"] + [("QuadMixed", 1244, 160)]
+                + [("QuadTracking", 0, 1344), ("EKFLeeLanded", 0, 2688)])
 
 
-@pytest.mark.parametrize("task,off", PARITY_CASES)
-def test_host_single_step_parity(task, off):
+@pytest.mark.parametrize("task,off,n", PARITY_CASES)
+def test_host_single_step_parity(task, off, n):
     """tests/test_gpu_env.py::test_single_step_parity on the host build, same tolerances."""
-    n = 160
     kw = {"convergence_time": 25} if task in ESTIMATOR else {}
     if off:
         kw.update(env_id_offset=off, num_envs_total=off + n + 1000)
