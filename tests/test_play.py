@@ -1,0 +1,69 @@
+"""``python -m ouzelum_amd.play``: the reference's ``train.py ... test=True`` play runs (EKFLeeExperiments.sh,
+metrics.sh) against the build, on the host build here (no GPU)."""
+import os
+
+import pytest
+
+from ouzelum_amd import play as P
+
+
+def test_parse_overrides_like_hydra():
+    cfg = P.parse_overrides(["task=EKFLeeLanded", "num_envs=512", "test=True", "headless=True", "max_iterations=1000",
+                             "+POMDP=flicker", "+pomdp_prob=0.3"])
+    assert cfg == {"task": "EKFLeeLanded", "num_envs": 512, "test": True, "headless": True, "max_iterations": 1000,
+                   "POMDP": "flicker", "pomdp_prob": 0.3}
+    with pytest.raises(ValueError):
+        P.parse_overrides(["task"])
+
+
+def test_ekf_experiment_play_run_writes_the_task_outputs(tmp_path):
+    """One line of EKFLeeExperiments.sh at a small size: the player runs until games_num episodes have finished,
+    prints rl_games' summary and leaves the trajectory CSVs of env 0 and the metrics counters behind."""
+    traj, met = tmp_path / "trajectories", tmp_path / "metrics"
+    args = ["task=EKFLeeLanded", "num_envs=64", "test=True", "headless=True", "max_iterations=1000", "+POMDP=flicker",
+            "+pomdp_prob=0.3", "sim_device=cpu", "games_num=64", "+max_episode_length=120", f"traj_dir={traj}",
+            f"metrics_dir={met}"]
+    with pytest.raises(ValueError, match="max_episode_length"):
+        P.main(args)   # not an override of the reference's command line
+    out = P.main([a for a in args if "max_episode_length" not in a] + ["games_num=8"])
+    assert out["games"] >= 8 and out["av_steps"] > 0 and out["tag"] == "flicker_0.3"
+    files = sorted(os.listdir(traj))
+    assert files and all(f.startswith("flicker_0.3_ep_") and f.endswith(".csv") for f in files)
+    with open(traj / files[0]) as fh:
+        assert fh.readline().strip() == "Position X,Position Y,Position Z"
+        assert len(fh.readline().split(",")) == 9      # EKFLeeLanded logs (pos, target, linvel)
+    assert (met / "flicker_0.3_ep_count.txt").read_text().strip() == str(out["episodes_logged"])
+    assert (met / "flicker_0.3.txt").read_text().strip() == str(out["landings"])
+
+
+def test_play_refuses_what_it_cannot_run(tmp_path):
+    base = ["num_envs=8", "sim_device=cpu", f"traj_dir={tmp_path}", f"metrics_dir={tmp_path}"]
+    with pytest.raises(ValueError, match="test=True"):
+        P.main(["task=EKFLeeLanded", "test=False"] + base)
+    with pytest.raises(ValueError, match="rl_games"):
+        P.main(["task=QuadFault", "test=True", "checkpoint=runs/Flicker_0.1/nn/Flicker_0.1.pth"] + base)
+
+
+@pytest.mark.parametrize("algo", ["rpo_lstm", "ppo"])
+def test_rl_task_plays_a_learner_checkpoint(tmp_path, algo):
+    """An RL task plays the mean action of a checkpoint saved by this build's learners (PPOLearner.save's files)."""
+    import torch
+    from ouzelum_amd import make
+    from ouzelum_amd.learners import PPOLearner
+    env = make(seed=0, task="QuadFault", num_envs=8, sim_device="cpu")
+    agent = PPOLearner(env.observation_space, env.action_space, 8, "cpu", recurrent=algo == "rpo_lstm")
+    prefix = str(tmp_path / "agent")
+    agent.save(prefix)
+    out = P.main(["task=QuadFault", "test=True", "num_envs=8", "sim_device=cpu", f"checkpoint={prefix}", f"algo={algo}",
+                  "games_num=8", f"traj_dir={tmp_path}/t", f"metrics_dir={tmp_path}/m"])
+    assert out["games"] >= 8 and torch.isfinite(torch.tensor(out["av_reward"]))
+
+
+@pytest.mark.gpu
+def test_ekf_experiment_play_run_on_the_gpu(tmp_path):
+    """The first line of EKFLeeExperiments.sh as written (512 envs, flicker 0.0) on the HIP env, until 600 games."""
+    out = P.main(["task=EKFLeeLanded", "num_envs=512", "test=True", "headless=True", "max_iterations=1000",
+                  "+POMDP=flicker", "+pomdp_prob=0.0", "games_num=600", f"traj_dir={tmp_path}/t",
+                  f"metrics_dir={tmp_path}/m"])
+    assert out["games"] >= 600 and out["av_steps"] > 0 and out["tag"] == "flicker_0"
+    assert os.listdir(tmp_path / "t") and (tmp_path / "m" / "flicker_0.txt").exists()
