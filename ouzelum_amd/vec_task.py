@@ -727,10 +727,14 @@ class QuadVecTask:
 
     # ----------------------------------------------------------- state I/O
     def _layout(self):
-        """What fixes the slot order of fstate / istate: the ABI's layout rules, the slot count and the shard's
-        place among the global ids (the mixed curriculum's slot map depends on env_id_offset)."""
+        """What fixes the slot order of fstate / istate: the ABI's layout rules, the slot count, the shard's place
+        among the global ids (the mixed curriculum's slot map depends on env_id_offset) and whether the slot map is
+        a trigger-class layout."""
         return {"abi": L.LAYOUT_VERSION, "slots": int(self.fstate.shape[0]) * L.TILE,
-                "env_id_offset": int(self.cfg.env_id_offset), "num_envs_total": int(self.cfg.num_envs_total)}
+                "env_id_offset": int(self.cfg.env_id_offset), "num_envs_total": int(self.cfg.num_envs_total),
+                # the slot map itself: a class layout of exactly k * 1344 envs (or OUZ_CLS_LARGE=1 above the
+                # latency regime) has the identity layout's slot count
+                "class_slots": self._env_slot is not None}
 
     def state_dict(self):
         """Env-state checkpoint (the reference never checkpoints env state).  The state is saved in

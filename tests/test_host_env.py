@@ -192,3 +192,16 @@ def test_host_vectask_surface():
     with pytest.raises(RuntimeError, match="track_episodes"):
         untracked.rollout(ring, 4, stats_out=torch.zeros(3, dtype=torch.float64))
     assert untracked.sim_step_count == step0
+
+
+def test_checkpoint_marker_names_the_slot_map():
+    """A class layout of exactly 2 x 1344 envs has the identity layout's slot count and shapes: the checkpoint's
+    layout marker carries the slot-map kind, so such a state is not loaded into the other layout silently."""
+    a = ouzelum_amd.make(seed=1, task="QuadTracking", num_envs=2688, sim_device="cpu")
+    b = ouzelum_amd.make(seed=1, task="LeeLanded", num_envs=2688, sim_device="cpu")
+    assert a._layout()["class_slots"] and not b._layout()["class_slots"]
+    sd = a.state_dict()
+    sd["layout"] = dict(sd["layout"], class_slots=False)
+    with pytest.raises(ValueError, match="layout"):
+        a.load_state_dict(sd)
+    a.load_state_dict(a.state_dict())
