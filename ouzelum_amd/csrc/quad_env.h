@@ -194,6 +194,7 @@ struct StepArgs {
   int32_t split;               // trigger-class layout: the split-wave estimator rollout (OUZ_SPLIT_PV; quad_pv_split.h)
   int32_t outw;                // latency-regime rollouts with an output wave (OUZ_OUT_WAVE; out_wave)
   int32_t xcd_pack;            // class layout above the latency regime: a class block's waves on one XCD (xcd_tile)
+  int32_t mix_split;           // mixed curriculum above the latency regime: one launch per task (mixed_task_tile)
   const ouz_dr_noise* drn;    // VecTask DR noise params in device memory: [0] observations, [1] actions
   int32_t drn_mask;            // bit 0: observation noise on, bit 1: action noise on
   float* trace;                // ouz_set_trace: [trace_cap][9] (p, target, v) of env trace_env

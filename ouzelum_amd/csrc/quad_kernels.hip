@@ -623,8 +623,23 @@ __host__ __device__ constexpr bool quad_lane_kernel(int task, bool cls) {
   return cls && (task == OUZ_TASK_EKF_LEE_LANDED || task == OUZ_TASK_TRACKING || task == OUZ_TASK_MIXED);
 }
 
+// The mixed curriculum above the latency regime, one launch per task (StepArgs.mix_split; MIXT kernels): a task's
+// launch steps only the 64-env tiles of its 1344-id chunks (chunk c runs task mixed_chunk_task(c), c % 3), with that
+// task's own kernel and register budget, instead of every wave carrying the estimator's (228 VGPRs: two waves per
+// SIMD for the LeeLanded / QuadFault chunks too).  Wave k of the launch of task TASK takes shard tile
+// mixed_task_tile(a, TASK, k), or -1 past the shard; the shard starts on a 64-env tile (env_offset % 64 == 0, checked
+// on the host), so every tile lies in one chunk.  Same per-env code as the one-launch kernel: bitwise its results.
+__device__ __forceinline__ int mixed_task_tile(const StepArgs& a, int task, int k) {
+  const uint32_t r = task == OUZ_TASK_LEE_LANDED ? 0u : (task == OUZ_TASK_TRACKING ? 1u : 2u);
+  const uint32_t g0 = a.env_offset / 64u, cf = g0 / (uint32_t)kTrigClasses;   // shard's first tile, its chunk
+  const uint32_t d = (r + 3u - cf % 3u) % 3u;                                   // first chunk of this task: cf + d
+  const uint32_t uk = (uint32_t)k, per = (uint32_t)kTrigClasses;
+  const int64_t t = (int64_t)((cf + d + 3u * (uk / per)) * per + uk % per) - (int64_t)g0;
+  return (t >= 0 && t < (int64_t)((a.n + 63) / 64)) ? (int)t : -1;
+}
+
 template <int TASK, bool MULTI, bool PRE = false, bool CLS = false, bool NTL = false, bool QUAD = false,
-          bool SPW = false, bool OWV = false>
+          bool SPW = false, bool OWV = false, bool MIXT = false>
 __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx, int K, const OutPtrs* outs,
                                           uint64_t out_stride, const RolloutStats* rst = nullptr,
                                           float* wrench = nullptr) {
@@ -750,6 +765,12 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
     return;
   }
   int i = blockIdx.x * step_block_for(a.n) + threadIdx.x;   // state slot
+  if constexpr (MIXT) {   // one task of the mixed curriculum: this wave's tile among that task's chunks
+    static_assert(!CLS && TASK != OUZ_TASK_MIXED, "a task launch of the mixed curriculum's identity layout");
+    const int t = (int)__builtin_amdgcn_readfirstlane(
+        (uint32_t)mixed_task_tile(a, TASK, (int)(blockIdx.x * (step_block_for(a.n) / 64) + (threadIdx.x >> 6))));
+    i = (t < 0 ? (a.n + 63) / 64 * 64 : t * 64) + (int)(threadIdx.x & 63u);
+  }
   if constexpr (CLS) {
     if (a.xcd_pack) {   // class layout above the latency regime: this wave's tile on its XCD (xcd_tile)
       const int t = xcd_tile(step_block_for(a.n) / 64, a.n_slots / kClassBlock);
@@ -807,17 +828,19 @@ __device__ __forceinline__ void step_body(const StepArgs& a, const StepCtx* ctx,
       run_env<CTRL_RL, TGT_GOAL, MULTI, PRE, false, NTL>(a, ctx, K, outs, out_stride, wave_lds, i, i, vr, OUZ_TASK_FAULT,
                                         direct, sm, &ls, wrench);
   }
-  if (sm) reduce_stats(*rst, (uint32_t)first >> 6, (uint32_t)((CLS ? a.n_slots : a.n) + 63) >> 6, ls);
+  if constexpr (!MIXT) {   // (a task launch of the split mixed curriculum never reduces statistics: rollout_impl)
+    if (sm) reduce_stats(*rst, (uint32_t)first >> 6, (uint32_t)((CLS ? a.n_slots : a.n) + 63) >> 6, ls);
+  }
 }
 
 // VecTask.step: one step, outputs into the env buffers.  Its arguments are StepArgs + one StepCtx
 // (~390 B): the host copies the argument block on every launch (≈0.6 us more host time per launch
 // for a 1.1 KB block, scripts/exp/launch_cost.hip), and at 4096 envs that host time is the bound.
-template <int TASK, bool CLS = false, bool NTL = false, bool QUAD = false>
+template <int TASK, bool CLS = false, bool NTL = false, bool QUAD = false, bool MIXT = false>
 __global__ void __launch_bounds__(kMaxBlock) quad_step_kernel(StepArgs a, StepCtx c) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(StepCtx) + 8)>();
   const OutPtrs env_out[2] = {OutPtrs{a.obs, a.rew, a.reset, a.timeouts}, OutPtrs{a.obs, a.rew, a.reset, a.timeouts}};
-  step_body<TASK, false, false, CLS, NTL, QUAD>(a, &c, 1, env_out, 0);
+  step_body<TASK, false, false, CLS, NTL, QUAD, false, false, MIXT>(a, &c, 1, env_out, 0);
 }
 
 // ouz_pre_physics: pre_physics_step alone, the body wrench to `wrench` [n][6].
@@ -834,11 +857,12 @@ __global__ void __launch_bounds__(kMaxBlock) quad_pre_kernel(StepArgs a, StepCtx
 // idle a third of the time; at two waves per SIMD the compiler spills ~90 VGPRs to scratch (L1/L2-resident) and
 // the rollout runs 10-12 % faster per step at 4 M envs (QuadTracking 410 -> 359 us, QuadMixed 380 -> 344:
 // profiles/r04/wide_rollout_ab.txt).
-template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false, bool OWV = false, int WPE = 1>
+template <int TASK, bool CLS = false, bool QUAD = false, bool SPW = false, bool OWV = false, int WPE = 1,
+          bool MIXT = false>
 __global__ void __launch_bounds__(kMaxBlock) __attribute__((amdgpu_waves_per_eu(WPE)))
 quad_rollout_kernel(StepArgs a, RolloutArgs r) {
   prefetch_kernargs<(int)(sizeof(StepArgs) + sizeof(RolloutArgs) + 8)>();
-  step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
+  step_body<TASK, true, false, CLS, false, QUAD, SPW, OWV, MIXT>(a, r.ctx, r.K, r.outs, r.out_stride, &r.stats);
 }
 #ifndef OUZ_EST_ROLLOUT_WPE
 #define OUZ_EST_ROLLOUT_WPE 2   // (A/B builds: -DOUZ_EST_ROLLOUT_WPE=3)
@@ -1294,6 +1318,10 @@ struct ouz_env {
   // 177 VGPRs, 2 waves per SIMD, against the step kernel's 5) and it runs ~2x slower per step than the
   // step kernel.  OUZ_ROLLOUT_STREAM=0/1 overrides.
   bool stream_rollout;
+  // The mixed curriculum's rollout above the latency regime as one launch per task (mixed_rollout: fused
+  // QuadTracking chunks, streamed LeeLanded / QuadFault chunks): OUZ_MIXED_SPLIT_ROLLOUT=1, opt-in -- measured 3 %
+  // slower than the one-launch fused kernel at 4 M envs (profiles/r05/mixed_split_rollout_probe.jsonl).
+  bool mix_split_rollout;
   // Whole-batch flicker coins of steps [mask_lo, mask_lo + kMaskCache): a pure function of (seed, task,
   // step), drawn on the host (6 Philox blocks per step for a flickering task, ~0.3 us).  Filled for the
   // next launch's steps right after a launch is submitted, while the GPU runs it, so a launch does not
@@ -1460,6 +1488,15 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
     if (a.cls) a.nt_loads = 0;   // the trigger-class layout (<= 64 K envs) has no such instantiation
   }
   {
+    // the mixed curriculum above the latency regime as one launch per task (mixed_task_tile); OUZ_MIXED_SPLIT=0
+    // keeps the one-launch kernel (bitwise the same results)
+    const char* ms = std::getenv("OUZ_MIXED_SPLIT");
+    a.mix_split = (cfg->task == OUZ_TASK_MIXED && !a.cls && a.env_offset % 64u == 0u &&
+                   (ms ? std::atoi(ms) != 0 : true)) ? 1 : 0;
+    const char* mr = std::getenv("OUZ_MIXED_SPLIT_ROLLOUT");
+    e->mix_split_rollout = a.mix_split && mr && std::atoi(mr) != 0;
+  }
+  {
     // the quad-lane estimator kernels (quad_pv_ql.h): bit-identical results, opt-in -- measured slower than the
     // one-lane kernels at 4096 envs (its LDS exchanges cost more than the f64 work they split)
     const char* ql = std::getenv("OUZ_QUAD_LANE");
@@ -1562,6 +1599,29 @@ static void launch_task(bool single, const StepArgs& a, const RolloutArgs& r, di
   else hipLaunchKernelGGL((quad_rollout_kernel<T, false>), g, b, 0, s, a, r);
 }
 
+// Waves of the launch of task T over the mixed curriculum's shard (mixed_task_tile): 21 per chunk of that task
+// that touches the shard (the first and last chunk may be partial: their waves past the shard exit at once).
+static int mixed_task_waves(const StepArgs& a, int task) {
+  const uint32_t r = task == OUZ_TASK_LEE_LANDED ? 0u : (task == OUZ_TASK_TRACKING ? 1u : 2u);
+  const uint32_t g0 = a.env_offset / 64u, cf = g0 / (uint32_t)kTrigClasses;
+  const uint32_t last = (g0 + (uint32_t)((a.n + 63) / 64) - 1u) / (uint32_t)kTrigClasses;   // last chunk touched
+  const uint32_t d = (r + 3u - cf % 3u) % 3u;
+  if (cf + d > last) return 0;
+  return (int)((last - cf - d) / 3u + 1u) * kTrigClasses;
+}
+
+extern "C++" template <int T>
+static void launch_mixed_task(bool single, const StepArgs& a, const RolloutArgs& r, dim3 b, hipStream_t s) {
+  const int waves = mixed_task_waves(a, T), wpb = (int)b.x / 64;
+  if (waves == 0) return;
+  const dim3 g((waves + wpb - 1) / wpb);
+  if (single && a.nt_loads) hipLaunchKernelGGL((quad_step_kernel<T, false, true, false, true>), g, b, 0, s, a, r.ctx[0]);
+  else if (single) hipLaunchKernelGGL((quad_step_kernel<T, false, false, false, true>), g, b, 0, s, a, r.ctx[0]);
+  else if (T == OUZ_TASK_TRACKING)
+    hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, false, OUZ_EST_ROLLOUT_WPE, true>), g, b, 0, s, a, r);
+  else hipLaunchKernelGGL((quad_rollout_kernel<T, false, false, false, false, 1, true>), g, b, 0, s, a, r);
+}
+
 static uint32_t cached_flicker_mask(ouz_env* env, int64_t step) {
   const int64_t off = step - env->mask_lo;
   if (off >= 0 && off < env->mask_n) return env->mask[off];
@@ -1615,6 +1675,17 @@ static int launch_steps(ouz_env* env, const float* ring, int32_t ring_len, int64
     g = dim3(8 * ((per_xcd + blk / 64 - 1) / (blk / 64)));
   }
   const bool single = K == 1 && !storage && !stats_mode;
+  if (env->cfg.task == OUZ_TASK_MIXED && a.mix_split && single) {
+    // VecTask.step as one launch per task over its chunks' tiles (mixed_task_tile).  A fused rollout keeps the
+    // one-launch kernel unless OUZ_MIXED_SPLIT_ROLLOUT=1 (rollout_impl -> mixed_rollout)
+    launch_mixed_task<OUZ_TASK_LEE_LANDED>(single, a, r, b, s);
+    launch_mixed_task<OUZ_TASK_TRACKING>(single, a, r, b, s);
+    launch_mixed_task<OUZ_TASK_FAULT>(single, a, r, b, s);
+    OUZ_LAUNCH_CHECK("quad_step_kernel (mixed, per task)");
+    env->step += K;
+    prefill_flicker_masks(env, env->step, kMaxRolloutChunk);
+    return OUZ_OK;
+  }
 #define OUZ_LAUNCH_TASK(T) launch_task<T>(single, a, r, g, b, s)
   switch (env->cfg.task) {
     case OUZ_TASK_OUZELUM: OUZ_LAUNCH_TASK(OUZ_TASK_OUZELUM); break;
@@ -1660,6 +1731,75 @@ int ouz_step_n(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_step
   return OUZ_OK;
 }
 
+// The mixed curriculum's rollout above the latency regime, one launch per task (StepArgs.mix_split): its
+// QuadTracking chunks as the fused estimator rollout (up to kMaxRolloutChunk steps per launch, state in registers);
+// its LeeLanded and QuadFault chunks streamed (one step launch per step, outputs straight into the storage rows),
+// the form those tasks take at this size on their own.  Every env runs the same per-env code as in the one-launch
+// kernel (equal within float tolerance, as the fused and streamed forms are).  The episode statistics are one
+// ouz_episode_stats launch after the steps, as for a streamed rollout.
+static int mixed_rollout(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out,
+                         float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int stats_mode,
+                         hipStream_t s) {
+  const bool store = obs_out != nullptr;
+  const size_t n = (size_t)env->cfg.num_envs;
+  const dim3 b(block_for((int)n));
+  const OutPtrs envout{env->buf.obs, env->buf.rew, env->buf.reset, env->buf.timeouts};
+  for (int32_t k0 = 0; k0 < n_steps; k0 += kMaxRolloutChunk) {
+    const int32_t K = (n_steps - k0) < kMaxRolloutChunk ? (n_steps - k0) : kMaxRolloutChunk;
+    const int64_t base = env->step;
+    RolloutArgs r;
+    std::memset(&r, 0, sizeof(r));
+    r.K = K;
+    for (int k = 0; k < K; ++k) {
+      r.ctx[k].step = (uint32_t)(base + k);
+      r.ctx[k].flick_mask = cached_flicker_mask(env, base + k);
+      r.ctx[k].actions = ring ? ring + (size_t)((k0 + k) % ring_len) * n * OUZ_NUM_ACT : nullptr;
+    }
+    r.outs[0] = store ? OutPtrs{obs_out + (size_t)k0 * n * OUZ_NUM_OBS, rew_out + (size_t)k0 * n,
+                                reset_out + (size_t)k0 * n, timeouts_out + (size_t)k0 * n} : envout;
+    r.outs[1] = envout;
+    r.out_stride = store ? (uint64_t)n : 0;
+    launch_mixed_task<OUZ_TASK_TRACKING>(false, env->args, r, b, s);
+    for (int32_t k = 0; k < K; ++k) {   // the streamed tasks, step by step (rollout_impl's streamed path)
+      const int32_t g = k0 + k;
+      StepArgs a = env->args;
+      if (store && g > 0) {
+        a.rst_in = reset_out + (size_t)(g - 1) * n;
+        a.to_in = timeouts_out + (size_t)(g - 1) * n;
+      }
+      if (store && g + 1 < n_steps) {
+        a.obs = obs_out + (size_t)g * n * OUZ_NUM_OBS;
+        a.rew = rew_out + (size_t)g * n;
+        a.reset = reset_out + (size_t)g * n;
+        a.timeouts = timeouts_out + (size_t)g * n;
+      }
+      RolloutArgs r1;
+      std::memset(&r1, 0, sizeof(r1));
+      r1.K = 1;
+      r1.ctx[0] = r.ctx[k];
+      launch_mixed_task<OUZ_TASK_LEE_LANDED>(true, a, r1, b, s);
+      launch_mixed_task<OUZ_TASK_FAULT>(true, a, r1, b, s);
+    }
+    OUZ_LAUNCH_CHECK("quad kernels (mixed rollout, per task)");
+    env->step = base + K;
+    prefill_flicker_masks(env, env->step, kMaxRolloutChunk);
+  }
+  if (store && n_steps > 0) {   // the streamed tasks' last step wrote the env buffers (the fused one wrote both)
+    const size_t last = (size_t)(n_steps - 1) * n;
+    const ouz_buffers& bf = env->buf;
+    int rc = hip_check(hipMemcpyAsync(obs_out + last * OUZ_NUM_OBS, bf.obs, n * OUZ_NUM_OBS * sizeof(float),
+                                      hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(rollout obs)");
+    if (!rc) rc = hip_check(hipMemcpyAsync(rew_out + last, bf.rew, n * sizeof(float), hipMemcpyDeviceToDevice, s),
+                            "hipMemcpyAsync(rollout rew)");
+    if (!rc) rc = hip_check(hipMemcpyAsync(reset_out + last, bf.reset, n * sizeof(int64_t), hipMemcpyDeviceToDevice, s),
+                            "hipMemcpyAsync(rollout reset)");
+    if (!rc) rc = hip_check(hipMemcpyAsync(timeouts_out + last, bf.timeouts, n, hipMemcpyDeviceToDevice, s),
+                            "hipMemcpyAsync(rollout timeouts)");
+    if (rc) return rc;
+  }
+  return stats_mode ? ouz_episode_stats(env, stats_out, stats_mode == 2 ? 1 : 0, s) : OUZ_OK;
+}
+
 static int rollout_impl(ouz_env* env, const float* ring, int32_t ring_len, int32_t n_steps, float* obs_out,
                         float* rew_out, int64_t* reset_out, uint8_t* timeouts_out, double* stats_out, int stats_mode,
                         void* stream, const char* fn) {
@@ -1669,6 +1809,9 @@ static int rollout_impl(ouz_env* env, const float* ring, int32_t ring_len, int32
   if (store && !(obs_out && rew_out && reset_out && timeouts_out))
     return fail(OUZ_ERR_INVALID, std::string(fn) + ": give all four storage pointers or none");
   const size_t n = (size_t)env->cfg.num_envs;
+  if (env->cfg.task == OUZ_TASK_MIXED && env->args.mix_split && env->mix_split_rollout)
+    return mixed_rollout(env, ring, ring_len, n_steps, obs_out, rew_out, reset_out, timeouts_out, stats_out,
+                         stats_mode, (hipStream_t)stream);
   if (env->stream_rollout) {
     // Streamed: step k reads the flags of row k - 1 and writes row k; the last step writes the env buffers,
     // which are then copied into the last row.  Bitwise K VecTask.step calls (the fused kernel is the same

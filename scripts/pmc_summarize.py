@@ -66,14 +66,58 @@ def avg_duration_us(stats_dir, kernel):
     return None, 0, None
 
 
+def _env_work(name):
+    # the env's own dispatches: its kernels and the runtime's device copies (the split mixed rollout's last-row
+    # copies), not torch's set-up kernels (the action ring's rand, zero fills)
+    return "ouz::" in name or "__amd_rocclr_copyBuffer" in name
+
+
+def mixed_split_counter(path_glob, counter, marker):
+    """The mixed curriculum above the latency regime runs one launch per task (quad_kernels.hip mix_split; a rollout
+    also runs its streamed tasks' step launches, the last-row copies and an episode-statistics launch): the summed
+    counter of all the env's dispatches per launch of the marker kernel (the QuadTracking chunks' kernel, one per
+    step or per rollout launch)."""
+    tot, marks = 0.0, 0
+    for f in glob.glob(path_glob, recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                if row.get("Counter_Name") != counter or not _env_work(name):
+                    continue
+                tot += float(row["Counter_Value"])
+                marks += marker in name
+    return (tot / marks, marks) if marks else (None, 0)
+
+
+def mixed_split_duration_us(stats_dir, marker):
+    """Summed rocprof duration of the env's dispatches per launch of the marker kernel."""
+    for f in glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(f) as fh:
+            rows = list(csv.DictReader(fh))
+        marks = sum(int(r["Calls"]) for r in rows if marker in r.get("Name", ""))
+        if marks:
+            tot = sum(float(r["TotalDurationNs"]) for r in rows if _env_work(r.get("Name", "")))
+            return tot / marks / 1e3, marks, os.path.relpath(f, stats_dir)
+    return None, 0, None
+
+
 def main():
     out, tag, task, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     mode = sys.argv[5] if len(sys.argv) > 5 else None
     base = os.path.join(out, f"pmc_{tag}_{mode}_{task}_{n}" if mode else f"pmc_{tag}_{task}_{n}")
     streamed = mode == "rollout" and n > 131072 and task not in ("EKFLeeLanded", "QuadTracking", "QuadMixed")
     kernel = "quad_rollout_kernel<" if mode == "rollout" and not streamed else "quad_step_kernel<"
-    fetch, nf = avg_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", kernel)
-    write, nw = avg_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", kernel)
+    # VecTask.step of the mixed curriculum above the latency regime is one launch per task (the default); its fused
+    # rollout one launch unless OUZ_MIXED_SPLIT_ROLLOUT=1
+    split = (task == "QuadMixed" and n > 65536 and os.environ.get("OUZ_MIXED_SPLIT", "1") != "0"
+             and (mode != "rollout" or os.environ.get("OUZ_MIXED_SPLIT_ROLLOUT", "0") != "0"))
+    marker = kernel + "3,"   # the QuadTracking chunks' kernel (OUZ_TASK_TRACKING = 3)
+    if split:
+        fetch, nf = mixed_split_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", marker)
+        write, nw = mixed_split_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", marker)
+    else:
+        fetch, nf = avg_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", kernel)
+        write, nw = avg_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", kernel)
     steps = 1
     if kernel == "quad_rollout_kernel<":   # kernel_driver.py's default launch length (bench.evidence_launch_steps)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -85,7 +129,10 @@ def main():
         res["lib_sha16"] = lib_sha16()
     except OSError:
         pass
-    us, calls, src = avg_duration_us(base + "_STATS", kernel)
+    if split:
+        res["mixed_split"] = ("per launch: every env dispatch (the three tasks' kernels, the streamed tasks' step "
+                              "launches, copies, statistics) summed over the QuadTracking chunks' launches")
+    us, calls, src = (mixed_split_duration_us if split else avg_duration_us)(base + "_STATS", marker if split else kernel)
     if us is not None:
         res.update({"rocprof_avg_us": us, "rocprof_calls": calls, "rocprof_stats_csv": src})
     if fetch is not None and write is not None:

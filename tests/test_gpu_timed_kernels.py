@@ -288,3 +288,67 @@ def test_cls_large_layout_is_bitwise_the_identity_layout(ouz, task, monkeypatch)
     assert torch.equal(outs[0][1], outs[1][1]) and float(outs[0][1][1]) > 0
     assert torch.equal(a.frows(0, L.F_COUNT), b.frows(0, L.F_COUNT))
     assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT))
+
+
+def test_mixed_split_matches_one_launch(ouz, monkeypatch):
+    """The mixed curriculum above 65 536 envs steps as one launch per task (StepArgs.mix_split: each task's kernel
+    and register budget over its own 1344-id chunks): bitwise the one-launch kernel (OUZ_MIXED_SPLIT=0), state and
+    outputs.  Its fused rollouts keep the one-launch kernel by default (bitwise); the opt-in split rollout
+    (OUZ_MIXED_SPLIT_ROLLOUT=1) gives the QuadTracking chunks' fused rollout bitwise the one-launch fused kernel's
+    on those envs and the LeeLanded / QuadFault chunks, streamed, bitwise the per-step launches (the one-launch
+    fused kernel differs from those within float tolerance only, checked by the large-N test above)."""
+    from ouzelum_amd import _lib as L
+    n = 70016 + 37
+    kw = dict(seed=31, task="QuadMixed", num_envs=n, sim_device="cuda:0", track_episodes=True,
+              convergence_time=10, max_episode_length=30)
+    d = ouz.make(**kw)                                        # the defaults: split steps, one-launch rollouts
+    monkeypatch.setenv("OUZ_MIXED_SPLIT_ROLLOUT", "1")
+    a = ouz.make(**kw)                                        # split steps and split rollouts (opt-in)
+    monkeypatch.delenv("OUZ_MIXED_SPLIT_ROLLOUT")
+    monkeypatch.setenv("OUZ_MIXED_SPLIT", "0")
+    one = ouz.make(**kw)
+    per = ouz.make(**kw)
+    monkeypatch.delenv("OUZ_MIXED_SPLIT")
+    ring = (torch.rand((RING, n, 4), device="cuda", generator=torch.Generator(device="cuda").manual_seed(5)) * 2
+            - 1).contiguous()
+    for env in (a, one, d):
+        env.rollout(ring, 20)                                # per-step launches
+    torch.cuda.synchronize()
+    assert torch.equal(a.fstate, one.fstate) and torch.equal(a.istate, one.istate)
+    assert torch.equal(a.obs_buf, one.obs_buf) and torch.equal(a.rew_buf, one.rew_buf)
+    assert torch.equal(a.reset_buf, one.reset_buf) and torch.equal(a.timeout_buf, one.timeout_buf)
+    per.rollout(ring, 20)
+    sts, stats = [], []
+    for env in (a, one, d):
+        st = storage_for(RING, n)
+        got = torch.zeros(3, dtype=torch.float64, device="cuda")
+        env.rollout(ring, RING, fused=True, storage=st, stats_out=got)
+        sts.append(st)
+        stats.append(got)
+    st = storage_for(RING, n)      # the same 16 steps as single launches, rows copied from the env buffers
+    for k in range(RING):
+        per.rollout(ring[k:k + 1].contiguous(), 1)
+        for row, buf in zip(st, (per.obs_buf, per.rew_buf, per.reset_buf, per.timeout_buf)):
+            row[k].copy_(buf)
+    sts.append(st)
+    stats.append(per.episode_stats())
+    torch.cuda.synchronize()
+    for x_one, x_def in zip(sts[1], sts[2]):                   # default rollout: the one-launch kernel
+        assert torch.equal(x_one, x_def)
+    assert torch.equal(d.fstate, one.fstate) and torch.equal(stats[1], stats[2])
+    sts, stats = [sts[0], sts[1], sts[3]], [stats[0], stats[1], stats[3]]
+    chunk_task = (torch.arange(n, device="cuda") // L.MIXED_CHUNK) % 3     # 0 LeeLanded, 1 QuadTracking, 2 QuadFault
+    trk, rest = chunk_task == 1, chunk_task != 1
+    for x_split, x_one, x_per in zip(*sts):
+        assert torch.equal(x_split[:, trk], x_one[:, trk])                # fused against fused
+        assert torch.equal(x_split[:, rest], x_per[:, rest])              # streamed against per-step
+    for buf in ("fstate", "istate"):
+        fs, fo, fp = getattr(a, buf), getattr(one, buf), getattr(per, buf)
+        tile_task = ((torch.arange(fs.shape[0], device="cuda") * L.TILE) // L.MIXED_CHUNK) % 3
+        assert torch.equal(fs[tile_task == 1], fo[tile_task == 1]) and torch.equal(fs[tile_task != 1], fp[tile_task != 1])
+    # the split rollout's statistics: ouz_episode_stats over every env after the steps.  Episodes finish in all
+    # three tasks (max_episode_length 30, mostly time-outs); the count agrees with the one-launch fused rollout's and
+    # the per-step path's up to the rare done flip of a fused estimator env (see the large-N test above)
+    c = [float(x[1]) for x in stats]
+    assert c[0] > 1000 and abs(c[0] - c[1]) <= 2 and abs(c[0] - c[2]) <= 2, c
+    a.check_health()
