@@ -66,10 +66,14 @@ def avg_duration_us(stats_dir, kernel):
     return None, 0, None
 
 
-def _env_work(name):
-    # the env's own dispatches: its kernels and the runtime's device copies (the split mixed rollout's last-row
-    # copies), not torch's set-up kernels (the action ring's rand, zero fills)
-    return "ouz::" in name or "__amd_rocclr_copyBuffer" in name
+def _env_work(name, marker):
+    # the dispatches of the workload: per step, the three tasks' step kernels; per rollout, also the streamed tasks'
+    # step launches, the last-row copies and the statistics launch -- not the env's creation (init_state_kernel)
+    # nor torch's set-up kernels (the action ring's rand, zero fills)
+    if marker.startswith("quad_step_kernel<"):
+        return "quad_step_kernel<" in name
+    return any(k in name for k in ("quad_rollout_kernel<", "quad_step_kernel<", "episode_stats",
+                                   "__amd_rocclr_copyBuffer"))
 
 
 def mixed_split_counter(path_glob, counter, marker):
@@ -82,7 +86,7 @@ def mixed_split_counter(path_glob, counter, marker):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 name = row.get("Kernel_Name", "")
-                if row.get("Counter_Name") != counter or not _env_work(name):
+                if row.get("Counter_Name") != counter or not _env_work(name, marker):
                     continue
                 tot += float(row["Counter_Value"])
                 marks += marker in name
@@ -96,7 +100,7 @@ def mixed_split_duration_us(stats_dir, marker):
             rows = list(csv.DictReader(fh))
         marks = sum(int(r["Calls"]) for r in rows if marker in r.get("Name", ""))
         if marks:
-            tot = sum(float(r["TotalDurationNs"]) for r in rows if _env_work(r.get("Name", "")))
+            tot = sum(float(r["TotalDurationNs"]) for r in rows if _env_work(r.get("Name", ""), marker))
             return tot / marks / 1e3, marks, os.path.relpath(f, stats_dir)
     return None, 0, None
 
