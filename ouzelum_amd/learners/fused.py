@@ -11,9 +11,13 @@
   a plain GEMM puts 16 output tiles on 256 CUs; splitting K into S slabs and summing
   gives 16·S workgroups.
 """
+import os
+
 import torch
 
 from .. import _lib as L
+
+_INPLACE_GATES = os.environ.get("OUZ_LSTM_INPLACE_GATES", "1") != "0"
 
 
 def _splits(k, n_out_tiles):
@@ -90,10 +94,19 @@ class LSTMSequence(torch.autograd.Function):
         cm = torch.empty((T + 1, B, H), device=dev)       # masked c entering each step
         torch.mul(h0, keep[0].unsqueeze(1), out=hm[0])
         torch.mul(c0, keep[0].unsqueeze(1), out=cm[0])
-        gates = torch.empty((B, G4), device=dev)
+        inplace = _INPLACE_GATES
+        gates = None if inplace else torch.empty((B, G4), device=dev)
         w_t = w_hh.t()
         for t in range(T):
-            torch.addmm(x_proj[t], hm[t], w_t, out=gates)
+            if inplace:
+                # the recurrent product accumulates onto the step's input projection in place (beta = 1, C = D):
+                # addmm with out= a separate buffer first copies the (B, 4H) projection into it, one runtime
+                # copy launch per step.  x_proj is this function's own temporary (SplitKLinear / addmm output)
+                # and is not saved for the backward pass.
+                gates = x_proj[t]
+                torch.addmm(gates, hm[t], w_t, out=gates)
+            else:
+                torch.addmm(x_proj[t], hm[t], w_t, out=gates)
             kn = keep[t + 1] if t + 1 < T else None
             L.check(L.lib.ouz_lstm_cell_fwd(gates.data_ptr(), cm[t].data_ptr(), _p(kn), act[t].data_ptr(),
                                             c_all[t].data_ptr(), hid[t].data_ptr(), hm[t + 1].data_ptr(),
