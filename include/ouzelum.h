@@ -60,10 +60,12 @@
 extern "C" {
 #endif
 
-#define OUZ_ABI_VERSION 4   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
+#define OUZ_ABI_VERSION 5   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
                                3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots;
                                4: physical domain randomisation (ouz_dr_physical, OUZ_I_RAND_STEP), DR noise
-                                  frequency (ouz_dr_noise.frequency) */
+                                  frequency (ouz_dr_noise.frequency);
+                               5: learner loss / trunk-backward kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss,
+                                  ouz_tanh_bwd_bias) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -402,6 +404,35 @@ int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* ke
 int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, const float* dhid, const float* G,
                       const float* dc_next, const float* keep_next, float* dgates, float* dc_prev, int32_t B, int32_t H,
                       void* stream);
+
+/* PPO losses of one minibatch, forward + gradient for a unit upstream gradient in one call (the losses end the
+ * graph).  Reductions are deterministic (fixed grid of OUZ_LOSS_BLOCKS per-block f64 partials summed in order).
+ * Workspace: OUZ_LOSS_WS_DOUBLES doubles, device memory, not kept between calls.
+ *
+ * Clipped policy loss (RPO-LSTM/agent.py:86-110; PPO/agent.py same lines): with lp = Normal(mean_z,
+ * exp(logstd)).log_prob(actions).sum(1) (torch's Normal: var = scale^2, log_scale = log(scale)), ratio =
+ * exp(lp - old_logp), A = advantages normalised by their mean and unbiased std + 1e-8 when norm_adv,
+ *   loss = mean(max(-A ratio, -A clamp(ratio, 1 - clip, 1 + clip))), approx_kl = mean((ratio - 1) - log ratio),
+ *   clipfrac = mean(|ratio - 1| > clip);
+ * dmean [n][4] = d loss / d mean_z and dlogstd [4] = d loss / d logstd (torch's maximum / clamp tie rules).
+ * mean_z (the RPO-perturbed mean), actions, dmean [n][OUZ_NUM_ACT] 16-byte aligned; logstd [OUZ_NUM_ACT];
+ * old_logp, advantages [n]; loss / approx_kl / clipfrac single floats. */
+#define OUZ_LOSS_BLOCKS 256
+#define OUZ_LOSS_WS_DOUBLES (10 * OUZ_LOSS_BLOCKS)
+int ouz_ppo_policy_loss(const float* mean_z, const float* logstd, const float* actions, const float* old_logp,
+                        const float* advantages, int32_t n, float clip, int32_t norm_adv, double* workspace,
+                        float* dmean, float* loss, float* approx_kl, float* clipfrac, float* dlogstd, void* stream);
+/* Value loss 0.5 * mean((values - returns)^2) (agent.py:104-105, clip_vloss False) and dvalues = (values -
+ * returns) / n. */
+int ouz_ppo_value_loss(const float* values, const float* returns, int32_t n, double* workspace, float* dvalues,
+                       float* loss, void* stream);
+
+/* Backward of y = tanh(x W^T + b) (the MLP trunks, RPO-LSTM/model.py:17-24,72-84): dz = dy (1 - y^2) and
+ * dbias = column sums of dz in one pass.  dy, y, dz [rows][cols] row-major, cols a power of two in [4, 1024];
+ * workspace OUZ_COLSUM_BLOCKS * cols floats; all 16-byte aligned.  Deterministic. */
+#define OUZ_COLSUM_BLOCKS 1024
+int ouz_tanh_bwd_bias(const float* dy, const float* y, int32_t rows, int32_t cols, float* workspace, float* dz,
+                      float* dbias, void* stream);
 
 #ifdef __cplusplus
 }

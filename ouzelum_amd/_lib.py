@@ -25,7 +25,7 @@ class OuzelumError(RuntimeError):
 
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
-ABI_VERSION = 4
+ABI_VERSION = 5
 LAYOUT_VERSION = 4  # the ABI version whose state-slot rules (include/ouzelum.h "State slots") the layout follows
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
@@ -142,7 +142,12 @@ SIGNATURES = {
     "ouz_pomdp_obs": (_I, [_P, _P, _I, _I, _I, _F, _U64, _I64, _U32, _P]),
     "ouz_lstm_cell_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ouz_lstm_cell_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "ouz_ppo_policy_loss": (_I, [_P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "ouz_ppo_value_loss": (_I, [_P, _P, _I, _P, _P, _P, _P]),
+    "ouz_tanh_bwd_bias": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
 }
+LOSS_WS_DOUBLES = 10 * 256      # OUZ_LOSS_WS_DOUBLES
+COLSUM_BLOCKS = 1024            # OUZ_COLSUM_BLOCKS
 
 
 # include/ouzelum_host.h, the same way: this table IS the list of symbols that header declares.

@@ -127,6 +127,226 @@ __global__ void __launch_bounds__(256) lstm_cell_bwd_kernel(const float* __restr
   dc_prev[idx] = dc * fg;
 }
 
+// ---------------------------------------------------------------------------
+// PPO losses of one minibatch (RPO-LSTM/agent.py:86-110, PPO/agent.py): the clipped policy loss with the
+// advantage normalisation, and the value loss, each as a forward that also writes the loss's gradient with
+// respect to its inputs for a unit upstream gradient (the loss is the end of the graph; the autograd
+// wrapper scales it).  torch's form is ~60 element-wise / reduction launches per minibatch (Normal.log_prob,
+// exp, max / clamp and their backward, six means); here 3 + 2.  Reductions are deterministic: per-block
+// f64 partials in a fixed grid (kLossBlocks), summed in block order by one finishing block.
+// ---------------------------------------------------------------------------
+constexpr int kLossThreads = 256;
+constexpr int kLossBlocks = OUZ_LOSS_BLOCKS;
+
+// sum over the block of v (f64), deterministic (fixed shuffle tree, then the 4 waves in order); all threads
+// receive the total
+__device__ double block_sum(double v, double* sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < kLossThreads / 64; ++k) t += sh[k];
+  return t;
+}
+
+__global__ void __launch_bounds__(kLossThreads) adv_moments_kernel(const float* __restrict__ adv, int n,
+                                                                   double* __restrict__ part) {
+  __shared__ double sh[kLossThreads / 64];
+  double s = 0.0, ss = 0.0;
+  for (int i = blockIdx.x * kLossThreads + threadIdx.x; i < n; i += kLossBlocks * kLossThreads) {
+    const double a = adv[i];
+    s += a;
+    ss += a * a;
+  }
+  s = block_sum(s, sh);
+  ss = block_sum(ss, sh);
+  if (threadIdx.x == 0) { part[2 * blockIdx.x] = s; part[2 * blockIdx.x + 1] = ss; }
+}
+
+// Normal(mean_z, exp(logstd)).log_prob(action).sum(1) as torch/distributions/normal.py forms it (scale = exp,
+// var = scale**2, log_scale = log(scale)), the ratio against the rollout's log-prob, the clipped surrogate and
+// its gradient, with torch's tie rule for maximum (equal arguments share the gradient) and clamp's inclusive
+// pass-through.  Per row: dmean (n, 4) for a unit upstream gradient; per block: loss, approx-kl and clip-count
+// sums and the four logstd gradient sums.
+__global__ void __launch_bounds__(kLossThreads) policy_loss_kernel(
+    const float* __restrict__ mean_z, const float* __restrict__ logstd, const float* __restrict__ act,
+    const float* __restrict__ old_logp, const float* __restrict__ adv, int n, float clip, int norm_adv,
+    const double* __restrict__ adv_part, float* __restrict__ dmean, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double sh[kLossThreads / 64];
+  float mu = 0.0f, den = 1.0f;
+  if (norm_adv) {   // (adv - adv.mean()) / (adv.std() + 1e-8), std unbiased; moments summed in block order
+    double s = 0.0, ss = 0.0;
+    for (int b = 0; b < kLossBlocks; ++b) { s += adv_part[2 * b]; ss += adv_part[2 * b + 1]; }
+    const double m = s / n;
+    const double var = (ss - s * m) / (double)(n - 1);
+    mu = (float)m;
+    den = (float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f;
+  }
+  float sd[OUZ_NUM_ACT], var[OUZ_NUM_ACT], lsc[OUZ_NUM_ACT];
+#pragma unroll
+  for (int j = 0; j < OUZ_NUM_ACT; ++j) {
+    sd[j] = expf(logstd[j]);
+    var[j] = sd[j] * sd[j];
+    lsc[j] = logf(sd[j]);
+  }
+  const float kLogSqrt2Pi = 0.918938533204672742f;
+  const float lo = 1.0f - clip, hi = 1.0f + clip;
+  const float inv_n = 1.0f / (float)n;
+  double s_loss = 0.0, s_kl = 0.0, s_cf = 0.0, s_ls[OUZ_NUM_ACT] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = blockIdx.x * kLossThreads + threadIdx.x; i < n; i += kLossBlocks * kLossThreads) {
+    const float4 m4 = reinterpret_cast<const float4*>(mean_z)[i];
+    const float4 a4 = reinterpret_cast<const float4*>(act)[i];
+    const float d[OUZ_NUM_ACT] = {a4.x - m4.x, a4.y - m4.y, a4.z - m4.z, a4.w - m4.w};
+    float lp = 0.0f;
+#pragma unroll
+    for (int j = 0; j < OUZ_NUM_ACT; ++j) lp += ((-(d[j] * d[j])) / (2.0f * var[j]) - lsc[j]) - kLogSqrt2Pi;
+    const float logratio = lp - old_logp[i];
+    const float ratio = expf(logratio);
+    const float a = norm_adv ? (adv[i] - mu) / den : adv[i];
+    const float na = -a;
+    const float l1 = na * ratio;
+    const float cr = fminf(fmaxf(ratio, lo), hi);
+    const float l2 = na * cr;
+    s_loss += (double)fmaxf(l1, l2);
+    s_kl += (double)((ratio - 1.0f) - logratio);
+    s_cf += fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
+    // d loss / d ratio for loss = mean(max(l1, l2)): maximum's backward gives each side the gradient where it is
+    // the larger and half of it on a tie; clamp passes its gradient where lo <= ratio <= hi
+    const float g = inv_n;
+    const float g1 = l1 > l2 ? g : (l1 == l2 ? g * 0.5f : 0.0f);
+    const float g2 = l2 > l1 ? g : (l1 == l2 ? g * 0.5f : 0.0f);
+    const float dratio = g1 * na + ((ratio >= lo && ratio <= hi) ? g2 * na : 0.0f);
+    const float dlp = dratio * ratio;   // exp's backward; logratio = lp - old
+    float4 dm;
+    dm.x = dlp * d[0] / var[0];
+    dm.y = dlp * d[1] / var[1];
+    dm.z = dlp * d[2] / var[2];
+    dm.w = dlp * d[3] / var[3];
+    reinterpret_cast<float4*>(dmean)[i] = dm;
+#pragma unroll
+    for (int j = 0; j < OUZ_NUM_ACT; ++j) s_ls[j] += (double)(dlp * (d[j] * d[j] / var[j] - 1.0f));
+  }
+  s_loss = block_sum(s_loss, sh);
+  s_kl = block_sum(s_kl, sh);
+  s_cf = block_sum(s_cf, sh);
+#pragma unroll
+  for (int j = 0; j < OUZ_NUM_ACT; ++j) s_ls[j] = block_sum(s_ls[j], sh);
+  if (threadIdx.x == 0) {
+    double* p = part + 8 * blockIdx.x;
+    p[0] = s_loss; p[1] = s_kl; p[2] = s_cf;
+#pragma unroll
+    for (int j = 0; j < OUZ_NUM_ACT; ++j) p[3 + j] = s_ls[j];
+  }
+}
+
+// 0.5 * mean((v - r)^2) (agent.py:104-105 with clip_vloss False) and dv = (v - r) / n for a unit upstream gradient
+__global__ void __launch_bounds__(kLossThreads) value_loss_kernel(const float* __restrict__ v,
+                                                                  const float* __restrict__ r, int n,
+                                                                  float* __restrict__ dv, double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double sh[kLossThreads / 64];
+  const float inv_n = 1.0f / (float)n;
+  double s = 0.0;
+  for (int i = blockIdx.x * kLossThreads + threadIdx.x; i < n; i += kLossBlocks * kLossThreads) {
+    const float d = v[i] - r[i];
+    s += (double)(d * d);
+    dv[i] = d * inv_n;
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) part[8 * blockIdx.x] = s;
+}
+
+// One block, one thread per partial block: out_k = (sum over blocks of part[8 b + k]) * scale for k < 3 (the
+// means); k >= 3: dlogstd[k - 3] = the sum itself (dlp already carries 1 / n).  Each sum is block_sum's fixed tree.
+static_assert(kLossBlocks == kLossThreads, "loss_finish_kernel: one thread per partial block");
+__global__ void __launch_bounds__(kLossThreads) loss_finish_kernel(const double* __restrict__ part, int nk,
+                                                                   double scale, float* __restrict__ o0,
+                                                                   float* __restrict__ o1, float* __restrict__ o2,
+                                                                   float* __restrict__ o3) {
+  __shared__ double sh[kLossThreads / 64];
+  const double* p = part + 8 * threadIdx.x;
+  for (int k = 0; k < nk; ++k) {
+    const double t = block_sum(p[k], sh);
+    if (threadIdx.x == 0) {
+      if (k == 0) *o0 = (float)(t * scale);
+      else if (k == 1) *o1 = (float)(t * scale);
+      else if (k == 2) *o2 = (float)(t * scale);
+      else o3[k - 3] = (float)t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Backward of y = tanh(x W^T + b) for the MLP trunks (RPO-LSTM/model.py:17-24,72-84): dz = dy (1 - y^2)
+// (torch's tanh_backward) and the bias gradient db = sum over rows of dz in the same pass, instead of a
+// tanh_backward launch and a column-sum launch that reads dz again.  Rows are split over a fixed grid
+// (deterministic: per-block column partials, then a column-wise sum in block order).
+// ---------------------------------------------------------------------------
+constexpr int kColBlocks = OUZ_COLSUM_BLOCKS;
+
+__global__ void __launch_bounds__(256) tanh_bwd_colsum_kernel(const float* __restrict__ dy,
+                                                              const float* __restrict__ y, float* __restrict__ dz,
+                                                              float* __restrict__ part, int rows, int cols) {
+#pragma clang fp contract(off)
+  __shared__ float4 sh[256];
+  const int cg = cols >> 2;                 // float4 column groups; 256 % cg == 0 (host-checked)
+  const int rp = 256 / cg;                  // rows per pass
+  const int c4 = threadIdx.x % cg, r0 = threadIdx.x / cg;
+  const int per = (rows + kColBlocks - 1) / kColBlocks;
+  const int rb = blockIdx.x * per, re = min(rows, rb + per);
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll 4
+  for (int r = rb + r0; r < re; r += rp) {
+    const size_t k = (size_t)r * cg + c4;
+    const float4 g = reinterpret_cast<const float4*>(dy)[k];
+    const float4 t = reinterpret_cast<const float4*>(y)[k];
+    float4 o;
+    o.x = g.x * (1.0f - t.x * t.x);
+    o.y = g.y * (1.0f - t.y * t.y);
+    o.z = g.z * (1.0f - t.z * t.z);
+    o.w = g.w * (1.0f - t.w * t.w);
+    reinterpret_cast<float4*>(dz)[k] = o;
+    acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  if (r0 == 0) {
+    for (int q = 1; q < rp; ++q) {
+      const float4 b = sh[q * cg + c4];
+      acc.x += b.x; acc.y += b.y; acc.z += b.z; acc.w += b.w;
+    }
+    reinterpret_cast<float4*>(part)[(size_t)blockIdx.x * cg + c4] = acc;
+  }
+}
+
+// db[c] = sum over the kColBlocks partial rows, 16 columns per block: the block's 16 row groups (threadIdx / 16)
+// each sum partial rows g, g + 16, ... in order (64 loads per thread, 8 in flight), then the 16 group sums are added
+// in group order
+__global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restrict__ part, int cols,
+                                                            float* __restrict__ db) {
+  __shared__ float sh[16][16];
+  const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+  const int c = blockIdx.x * 16 + l;
+  float t = 0.0f;
+  if (c < cols) {
+#pragma unroll 8
+    for (int b = g; b < kColBlocks; b += 16) t += part[(size_t)b * cols + c];
+  }
+  sh[g][l] = t;
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    float s = sh[0][l];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) s += sh[q][l];
+    db[c] = s;
+  }
+}
+
 inline int grid(int n, int b) { return (n + b - 1) / b; }
 
 int launch_status(const char* what) {
@@ -196,6 +416,51 @@ int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, c
   hipLaunchKernelGGL(lstm_cell_bwd_kernel, dim3(grid(B * H, 256)), dim3(256), 0, (hipStream_t)stream, act, c, c_prev_m,
                      dhid, G, dc_next, keep_next, dgates, dc_prev, B, H);
   return launch_status("lstm_cell_bwd_kernel");
+}
+
+int ouz_ppo_policy_loss(const float* mean_z, const float* logstd, const float* actions, const float* old_logp,
+                        const float* advantages, int32_t n, float clip, int32_t norm_adv, double* workspace,
+                        float* dmean, float* loss, float* approx_kl, float* clipfrac, float* dlogstd, void* stream) {
+  if (n <= 0 || (norm_adv && n < 2)) return set_error(OUZ_ERR_INVALID, "ouz_ppo_policy_loss: n must be > 0 (> 1 with norm_adv)");
+  if (!mean_z || !logstd || !actions || !old_logp || !advantages || !workspace || !dmean || !loss || !approx_kl ||
+      !clipfrac || !dlogstd)
+    return set_error(OUZ_ERR_INVALID, "ouz_ppo_policy_loss: null buffer");
+  if (((reinterpret_cast<uintptr_t>(mean_z) | reinterpret_cast<uintptr_t>(actions) | reinterpret_cast<uintptr_t>(dmean)) & 15u))
+    return set_error(OUZ_ERR_INVALID, "ouz_ppo_policy_loss: mean_z / actions / dmean must be 16-byte aligned");
+  const hipStream_t s = (hipStream_t)stream;
+  double* adv_part = workspace;
+  double* part = workspace + 2 * kLossBlocks;
+  if (norm_adv) hipLaunchKernelGGL(adv_moments_kernel, dim3(kLossBlocks), dim3(kLossThreads), 0, s, advantages, n, adv_part);
+  hipLaunchKernelGGL(policy_loss_kernel, dim3(kLossBlocks), dim3(kLossThreads), 0, s, mean_z, logstd, actions, old_logp,
+                     advantages, n, clip, norm_adv, adv_part, dmean, part);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(kLossThreads), 0, s, part, 3 + OUZ_NUM_ACT, 1.0 / (double)n, loss,
+                     approx_kl, clipfrac, dlogstd);
+  return launch_status("policy_loss_kernel");
+}
+
+int ouz_ppo_value_loss(const float* values, const float* returns, int32_t n, double* workspace, float* dvalues,
+                       float* loss, void* stream) {
+  if (n <= 0) return set_error(OUZ_ERR_INVALID, "ouz_ppo_value_loss: n must be > 0");
+  if (!values || !returns || !workspace || !dvalues || !loss) return set_error(OUZ_ERR_INVALID, "ouz_ppo_value_loss: null buffer");
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(value_loss_kernel, dim3(kLossBlocks), dim3(kLossThreads), 0, s, values, returns, n, dvalues, workspace);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(kLossThreads), 0, s, workspace, 1, 0.5 / (double)n, loss, nullptr, nullptr,
+                     nullptr);
+  return launch_status("value_loss_kernel");
+}
+
+int ouz_tanh_bwd_bias(const float* dy, const float* y, int32_t rows, int32_t cols, float* workspace, float* dz,
+                      float* dbias, void* stream) {
+  if (rows <= 0 || cols <= 0 || cols % 4 || cols > 1024 || 256 % (cols / 4))
+    return set_error(OUZ_ERR_INVALID, "ouz_tanh_bwd_bias: rows > 0 and cols a power of two in [4, 1024]");
+  if (!dy || !y || !workspace || !dz || !dbias) return set_error(OUZ_ERR_INVALID, "ouz_tanh_bwd_bias: null buffer");
+  if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(dz) |
+        reinterpret_cast<uintptr_t>(workspace)) & 15u))
+    return set_error(OUZ_ERR_INVALID, "ouz_tanh_bwd_bias: buffers must be 16-byte aligned");
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(kColBlocks), dim3(256), 0, s, dy, y, dz, workspace, rows, cols);
+  hipLaunchKernelGGL(colsum_finish_kernel, dim3(grid(cols, 16)), dim3(256), 0, s, workspace, cols, dbias);
+  return launch_status("tanh_bwd_colsum_kernel");
 }
 
 }  // extern "C"

@@ -10,6 +10,11 @@
   (32 768 at the reference's 16 x 4096 minibatch halves) and a small output (512 x 256):
   a plain GEMM puts 16 output tiles on 256 CUs; splitting K into S slabs and summing
   gives 16·S workgroups.
+* ``LinearTanh``: Linear + Tanh of the MLP trunks with the backward's tanh' and bias
+  gradient in one HIP pass (``ouz_tanh_bwd_bias``) instead of tanh_backward + a column sum.
+* ``PolicyLoss`` / ``ValueLoss``: the PPO losses of a minibatch (``RPO-LSTM/agent.py:86-110``)
+  as one HIP forward each that also writes the loss's input gradients (``ouz_ppo_policy_loss``,
+  ``ouz_ppo_value_loss``), replacing ~60 element-wise and reduction launches per minibatch.
 """
 import os
 
@@ -18,6 +23,7 @@ import torch
 from .. import _lib as L
 
 _INPLACE_GATES = os.environ.get("OUZ_LSTM_INPLACE_GATES", "1") != "0"
+_FUSED_TANH = os.environ.get("OUZ_FUSED_TANH", "1") != "0"
 
 
 def _splits(k, n_out_tiles):
@@ -57,18 +63,126 @@ class SplitKLinear(torch.autograd.Function):
         return dx, dw, db
 
 
+class LinearTanh(torch.autograd.Function):
+    """y = tanh(x Wᵀ + b); backward: dz = dy (1 - y²) and db = Σ_rows dz in one HIP pass, then dx = dz W and the
+    split-K dW = dzᵀ x."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        y = torch.addmm(bias, x, weight.t())
+        torch.tanh_(y)
+        ctx.save_for_backward(x, weight, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        rows, cols = y.shape
+        dz = torch.empty_like(y)
+        db = torch.empty(cols, device=y.device)
+        ws = torch.empty(L.COLSUM_BLOCKS * cols, device=y.device)
+        L.check(L.lib.ouz_tanh_bwd_bias(dy.data_ptr(), y.data_ptr(), rows, cols, ws.data_ptr(), dz.data_ptr(),
+                                        db.data_ptr(), L.stream_ptr(y.device)), "ouz_tanh_bwd_bias")
+        dx = dz.mm(weight) if ctx.needs_input_grad[0] else None
+        dw = splitk_wgrad(dz, x.contiguous()) if ctx.needs_input_grad[1] else None
+        return dx, dw, db
+
+
+def _fused_ok(x, min_rows):
+    return x.is_cuda and x.dim() == 2 and x.shape[0] >= min_rows and torch.is_grad_enabled()
+
+
 def linear(x, layer, min_rows=8192):
     """nn.Linear forward; rows >= min_rows on a GPU take the split-K weight gradient."""
-    if x.is_cuda and x.dim() == 2 and x.shape[0] >= min_rows and torch.is_grad_enabled():
+    if _fused_ok(x, min_rows):
         return SplitKLinear.apply(x, layer.weight, layer.bias)
     return torch.nn.functional.linear(x, layer.weight, layer.bias)
 
 
-def run_mlp(seq, x):
-    """Forward through an nn.Sequential of Linear / activation modules using ``linear``."""
-    for m in seq:
-        x = linear(x, m) if isinstance(m, torch.nn.Linear) else m(x)
+def _tanh_fusable(layer, x, min_rows):
+    cols = layer.out_features
+    return (_FUSED_TANH and layer.bias is not None and _fused_ok(x, min_rows) and 4 <= cols <= 1024
+            and cols & (cols - 1) == 0)
+
+
+def run_mlp(seq, x, min_rows=8192):
+    """Forward through an nn.Sequential of Linear / activation modules using ``linear``; a Linear followed by a
+    Tanh becomes one ``LinearTanh`` where its rows and width allow."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, torch.nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.Tanh)
+                and _tanh_fusable(m, x, min_rows)):
+            x = LinearTanh.apply(x, m.weight, m.bias)
+            i += 2
+            continue
+        x = linear(x, m, min_rows) if isinstance(m, torch.nn.Linear) else m(x)
+        i += 1
     return x
+
+
+class PolicyLoss(torch.autograd.Function):
+    """(mean_z (n, 4), logstd (1, 4), actions (n, 4), old_logp (n,), advantages (n,), clip, norm_adv) ->
+    (pg_loss, approx_kl, clipfrac), 0-dim; only pg_loss is differentiable.  ``mean_z`` is the policy mean with
+    RPO's noise already added (model.py:61-64)."""
+
+    @staticmethod
+    def forward(ctx, mean_z, logstd, actions, old_logp, adv, clip, norm_adv):
+        dev = mean_z.device
+        n = mean_z.shape[0]
+        # contiguous f32 operands held in locals until the launch is queued
+        mz, ls, act, old, a = (t.detach().contiguous() for t in (mean_z, logstd, actions, old_logp, adv))
+        for t, name in ((mz, "mean_z"), (ls, "logstd"), (act, "actions"), (old, "old_logp"), (a, "advantages")):
+            L.require_hip_tensor(t, name)
+            if t.dtype != torch.float32:
+                raise ValueError(f"PolicyLoss: {name} must be float32")
+        if mz.shape != (n, L.NUM_ACT) or act.shape != (n, L.NUM_ACT) or ls.numel() != L.NUM_ACT \
+                or old.numel() != n or a.numel() != n:
+            raise ValueError("PolicyLoss: mean_z / actions (n, 4), logstd 4 values, old_logp / advantages n values")
+        dmean = torch.empty_like(mz)
+        loss, kl, cf = (torch.empty((), device=dev) for _ in range(3))
+        dls = torch.empty(logstd.shape, device=dev)
+        ws = torch.empty(L.LOSS_WS_DOUBLES, dtype=torch.float64, device=dev)
+        L.check(L.lib.ouz_ppo_policy_loss(mz.data_ptr(), ls.data_ptr(), act.data_ptr(), old.data_ptr(), a.data_ptr(),
+                                          n, float(clip), int(bool(norm_adv)), ws.data_ptr(), dmean.data_ptr(),
+                                          loss.data_ptr(), kl.data_ptr(), cf.data_ptr(), dls.data_ptr(),
+                                          L.stream_ptr(dev)), "ouz_ppo_policy_loss")
+        ctx.save_for_backward(dmean, dls)
+        ctx.mark_non_differentiable(kl, cf)
+        ctx.set_materialize_grads(False)
+        return loss, kl, cf
+
+    @staticmethod
+    def backward(ctx, g, _gkl, _gcf):
+        dmean, dls = ctx.saved_tensors
+        return dmean * g, dls * g, None, None, None, None, None
+
+
+class ValueLoss(torch.autograd.Function):
+    """(values (n,), returns (n,)) -> 0.5 * mean((values - returns)²), 0-dim (agent.py:104-105)."""
+
+    @staticmethod
+    def forward(ctx, values, returns):
+        dev = values.device
+        v, r = values.detach().contiguous(), returns.detach().contiguous()
+        L.require_hip_tensor(v, "values")
+        L.require_hip_tensor(r, "returns")
+        if v.dim() != 1 or r.shape != v.shape or v.dtype != torch.float32 or r.dtype != torch.float32:
+            raise ValueError("ValueLoss: values and returns (n,) float32")
+        dv = torch.empty_like(v)
+        loss = torch.empty((), device=dev)
+        ws = torch.empty(L.LOSS_WS_DOUBLES, dtype=torch.float64, device=dev)
+        L.check(L.lib.ouz_ppo_value_loss(v.data_ptr(), r.data_ptr(), v.shape[0], ws.data_ptr(), dv.data_ptr(),
+                                         loss.data_ptr(), L.stream_ptr(dev)), "ouz_ppo_value_loss")
+        ctx.save_for_backward(dv)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dv,) = ctx.saved_tensors
+        return dv * g, None
 
 
 def _p(t):
@@ -81,6 +195,7 @@ class LSTMSequence(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_proj, h0, c0, keep, w_hh):
+        ctx.set_materialize_grads(False)     # unused h_T / c_T come back as None, not zero-filled tensors
         T, B, G4 = x_proj.shape
         H = G4 // 4
         dev = x_proj.device

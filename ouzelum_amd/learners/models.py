@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 from torch.distributions.normal import Normal
 
-from .fused import LSTMSequence, SplitKLinear, run_mlp
+from .fused import LSTMSequence, SplitKLinear, linear, run_mlp
 
 
 def layer_init(layer, std=math.sqrt(2), bias_const=0.0):
@@ -53,6 +53,10 @@ class MLPActor(nn.Module):
     def forward(self, state, action=None, eps=None):
         mean = run_mlp(self.actor_mean, state)
         return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps)
+
+    def update_mean(self, state):
+        """The mean the policy update scores its actions under (RPO's noise added), for ``fused.PolicyLoss``."""
+        return _rpo_mean(run_mlp(self.actor_mean, state), self.rpo_alpha)
 
 
 class LSTMActor(nn.Module):
@@ -113,8 +117,22 @@ class LSTMActor(nn.Module):
 
     def forward(self, state, lstm_state, done, action=None, eps=None):
         hidden, lstm_state = self.get_states(state, lstm_state, done)
-        mean = self.actor_mean(hidden)    # 128 -> 4: too small for the split-K path
+        mean = linear(hidden, self.actor_mean)
         return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps), lstm_state)
+
+    def update_mean(self, state, lstm_state, done):
+        """The mean the policy update scores its actions under (RPO's noise added, model.py:61-64), for
+        ``fused.PolicyLoss``."""
+        hidden, _ = self.get_states(state, lstm_state, done)
+        # 128 -> 4 over T·B rows: the split-K weight gradient (a plain GEMM puts its 4 x 128 output on one tile)
+        return _rpo_mean(linear(hidden, self.actor_mean), self.rpo_alpha)
+
+
+def _rpo_mean(mean, rpo_alpha):
+    # the same draw, in the same order, as _policy_head's
+    if rpo_alpha > 0.0:
+        mean = mean + torch.empty_like(mean).uniform_(-rpo_alpha, rpo_alpha)
+    return mean
 
 
 def _policy_head(mean, logstd, action, rpo_alpha, eps=None):
@@ -128,8 +146,7 @@ def _policy_head(mean, logstd, action, rpo_alpha, eps=None):
         probs = Normal(mean, std, validate_args=False)
         action = mean + std * (torch.randn_like(mean) if eps is None else eps)
     else:
-        if rpo_alpha > 0.0:   # RPO: perturb the mean for the policy update (RPO-LSTM/model.py:61-64)
-            mean = mean + torch.empty_like(mean).uniform_(-rpo_alpha, rpo_alpha)
+        mean = _rpo_mean(mean, rpo_alpha)   # RPO: perturb the mean for the policy update (RPO-LSTM/model.py:61-64)
         probs = Normal(mean, std, validate_args=False)
     return action, probs.log_prob(action).sum(1), probs.entropy().sum(1)
 

@@ -69,9 +69,25 @@ def test_header_constants_match_python_mirror(L):
     assert int(defines["OUZ_ABI_VERSION"]) == L.ABI_VERSION == L.lib.ouz_abi_version()
     assert int(defines["OUZ_TASK_MIXED"]) == L.TASK_MIXED and int(defines["OUZ_NUM_TASKS"]) == L.NUM_TASKS
     assert int(defines["OUZ_POMDP_FLICKER_NOISE"]) == L.POMDP_FLICKER_NOISE
+    assert 10 * int(defines["OUZ_LOSS_BLOCKS"]) == L.LOSS_WS_DOUBLES
+    assert int(defines["OUZ_COLSUM_BLOCKS"]) == L.COLSUM_BLOCKS
     enums = dict(re.findall(r"(OUZ_[FI]_\w+) = (\d+)", src))
     for k, v in enums.items():
         assert getattr(L, k[4:]) == int(v), k
+
+
+def test_learner_loss_entry_points_validate_without_gpu(L):
+    """The loss / trunk-backward entry points refuse bad sizes and null buffers before launching anything."""
+    assert L.lib.ouz_ppo_policy_loss(*([None] * 5), 1, 0.2, 1, *([None] * 7)) == -1      # norm_adv needs n > 1
+    assert b"n must be" in L.lib.ouz_last_error()
+    assert L.lib.ouz_ppo_policy_loss(*([None] * 5), 8, 0.2, 0, *([None] * 7)) == -1
+    assert b"null buffer" in L.lib.ouz_last_error()
+    assert L.lib.ouz_ppo_value_loss(None, None, 0, None, None, None, None) == -1
+    assert L.lib.ouz_tanh_bwd_bias(None, None, 16, 12, None, None, None, None) == -1      # 12 columns
+    assert b"power of two" in L.lib.ouz_last_error()
+    assert L.lib.ouz_tanh_bwd_bias(None, None, 16, 2048, None, None, None, None) == -1
+    assert L.lib.ouz_tanh_bwd_bias(None, None, 16, 256, None, None, None, None) == -1
+    assert b"null buffer" in L.lib.ouz_last_error()
 
 
 def test_struct_layout(L):

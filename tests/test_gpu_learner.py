@@ -227,3 +227,118 @@ def test_graph_replay_policy_follows_the_runtime_not_torch_flag():
                              timeout=120)
         assert out.returncode == 0, (name, out.stderr[-2000:])
         assert out.stdout.strip().splitlines()[-1] == want, (name, out.stdout)
+
+
+def _torch_policy_loss(mean_z, logstd, actions, old_logp, adv, clip, norm_adv):
+    """The reference's clipped policy loss (RPO-LSTM/agent.py:86-110) in torch f32, from the RPO-perturbed mean."""
+    from torch.distributions.normal import Normal
+    probs = Normal(mean_z, torch.exp(logstd.expand_as(mean_z)), validate_args=False)
+    logratio = probs.log_prob(actions).sum(1) - old_logp
+    ratio = logratio.exp()
+    approx_kl = ((ratio - 1) - logratio).mean()
+    clipfrac = ((ratio - 1.0).abs() > clip).float().mean()
+    if norm_adv:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    pg = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+    return pg, approx_kl, clipfrac
+
+
+@pytest.mark.parametrize("n,norm_adv", [(65536, True), (1000, True), (4099, False), (2, True)])
+def test_policy_loss_kernel_matches_torch(n, norm_adv):
+    """ouz_ppo_policy_loss (loss, approx-kl, clip fraction, d/d mean, d/d logstd) against torch autograd through
+    the reference formula.  Old log-probs are set so that ratios fall inside, on both sides of and exactly at the
+    clip range (ties of the max, clamp's inclusive edges).  Tolerance: f32 reductions in another order."""
+    from ouzelum_amd.learners.fused import PolicyLoss
+    g = torch.Generator(device="cuda").manual_seed(n)
+    mean = torch.randn(n, 4, device="cuda", generator=g) * 0.5
+    logstd = (torch.randn(1, 4, device="cuda", generator=g) * 0.3)
+    act = (mean + torch.randn(n, 4, device="cuda", generator=g) * 0.7).clamp(-1, 1)
+    adv = torch.randn(n, device="cuda", generator=g) * 2.0 + 0.3
+    with torch.no_grad():
+        from torch.distributions.normal import Normal
+        lp = Normal(mean, torch.exp(logstd.expand_as(mean))).log_prob(act).sum(1)
+    shift = torch.randn(n, device="cuda", generator=g) * 0.3
+    shift[::7] = 0.0                                    # ratio exactly 1
+    old = lp - shift
+    out = []
+    for fn in (PolicyLoss.apply, _torch_policy_loss):
+        m = mean.clone().requires_grad_(True)
+        ls = logstd.clone().requires_grad_(True)
+        pg, kl, cf = fn(m, ls, act, old, adv, 0.2, norm_adv)
+        (pg * 1.5).backward()
+        out.append((pg.detach(), kl, cf, m.grad, ls.grad))
+    (pg0, kl0, cf0, dm0, dl0), (pg1, kl1, cf1, dm1, dl1) = out
+    torch.testing.assert_close(pg0, pg1, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(kl0, kl1, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(cf0, cf1, rtol=0, atol=1.5 / n)     # a ratio within one ulp of the clip edge
+    torch.testing.assert_close(dm0, dm1, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(dl0, dl1, rtol=1e-4, atol=1e-6)
+
+
+def test_value_loss_kernel_matches_torch():
+    from ouzelum_amd.learners.fused import ValueLoss
+    g = torch.Generator(device="cuda").manual_seed(5)
+    v0 = torch.randn(65536 + 13, device="cuda", generator=g) * 3
+    r = torch.randn(65536 + 13, device="cuda", generator=g) * 3
+    out = []
+    for fn in (ValueLoss.apply, lambda v, r: 0.5 * ((v - r) ** 2).mean()):
+        v = v0.clone().requires_grad_(True)
+        loss = fn(v, r)
+        (loss * 2.0).backward()
+        out.append((loss.detach(), v.grad))
+    torch.testing.assert_close(out[0][0], out[1][0], rtol=1e-5, atol=0)
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=1e-5, atol=1e-9)
+    with pytest.raises(ValueError):
+        ValueLoss.apply(v0.double(), r.double())
+
+
+@pytest.mark.parametrize("rows,k,cols", [(65536, 13, 512), (16384, 512, 256), (10001, 64, 4), (8192, 256, 1024)])
+def test_linear_tanh_matches_torch(rows, k, cols):
+    """fused.LinearTanh (ouz_tanh_bwd_bias: tanh' and the bias gradient in one pass) against nn.Linear + Tanh."""
+    from ouzelum_amd.learners.fused import LinearTanh
+    torch.manual_seed(rows + cols)
+    lin = torch.nn.Linear(k, cols).cuda()
+    x0 = torch.randn(rows, k, device="cuda")
+    w_out = torch.randn(rows, cols, device="cuda")
+    res = []
+    for fused in (True, False):
+        lin.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        y = LinearTanh.apply(x, lin.weight, lin.bias) if fused else torch.tanh(lin(x))
+        (y * w_out).sum().backward()
+        res.append((y.detach(), x.grad, lin.weight.grad.clone(), lin.bias.grad.clone()))
+    for a, b, name in zip(res[0], res[1], ("y", "dx", "dW", "db")):
+        err = float((a - b).abs().max() / b.abs().max().clamp_min(1e-6))
+        assert err < 2e-5, (name, err)
+
+
+@pytest.mark.parametrize("recurrent", [True, False])
+def test_fused_update_matches_torch_losses(recurrent, monkeypatch):
+    """One PPO minibatch through the HIP losses (default) and through the torch form (OUZ_FUSED_LOSS=0): same
+    weights and RNG, so the same RPO noise and permutation; losses and the clipped gradients agree."""
+    from ouzelum_amd.learners import PPOLearner
+    from ouzelum_amd.spaces import Box
+    N, T = 1024, 16
+    obs_s, act_s = Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))
+    g = torch.Generator(device="cuda").manual_seed(11)
+    obs = torch.randn(T, N, 13, device="cuda", generator=g)
+    acts = torch.rand(T, N, 4, device="cuda", generator=g) * 2 - 1
+    rew = torch.randn(T, N, device="cuda", generator=g)
+    dones = (torch.rand(T, N, device="cuda", generator=g) < 0.05).float()
+    logp = -torch.rand(T, N, device="cuda", generator=g) * 4 - 2
+    results = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("OUZ_FUSED_LOSS", flag)
+        torch.manual_seed(3)
+        ag = PPOLearner(obs_s, act_s, N, "cuda", recurrent=recurrent, num_minibatches=1, update_epochs=1)
+        init = ag.initial_state()
+        stats = ag.train(obs, obs, acts, obs[-1], dones[-1], init, logp, rew, dones)
+        grads = {f"a.{k}": p.grad.clone() for k, p in ag.actor.named_parameters() if p.grad is not None}
+        grads.update({f"c.{k}": p.grad.clone() for k, p in ag.critic.named_parameters() if p.grad is not None})
+        results.append(({k: float(v) for k, v in stats.items()}, grads))
+    (s0, g0), (s1, g1) = results
+    for k in ("pg_loss", "v_loss", "approx_kl", "clipfrac"):
+        assert abs(s0[k] - s1[k]) <= 1e-4 * abs(s1[k]) + 2e-6, (k, s0[k], s1[k])
+    assert set(g0) == set(g1)
+    errs = {k: float((g0[k] - g1[k]).abs().max() / g1[k].abs().max().clamp_min(1e-8)) for k in g1}
+    assert max(errs.values()) < 1e-3, errs
