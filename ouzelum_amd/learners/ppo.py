@@ -29,6 +29,7 @@ import torch.nn as nn
 
 from .. import _lib as L
 from .fused import PolicyLoss, ValueLoss
+from .gemm_tuning import enable_tuned_gemms
 from .models import Critic, LSTMActor, MLPActor
 
 
@@ -112,6 +113,7 @@ class PPOLearner:
         self.minibatch_size = self.batch_size // num_minibatches
         if recurrent and num_envs % num_minibatches:
             raise ValueError("num_envs must divide into the minibatches")   # agent.py:72
+        enable_tuned_gemms(self.device)       # per-shape GEMM solutions (gemm_tuning.py); OUZ_TUNABLEOP=0: off
         self.actor = (LSTMActor(observation_space, action_space) if recurrent
                       else MLPActor(observation_space, action_space)).to(self.device)
         self.critic = Critic(observation_space).to(self.device)

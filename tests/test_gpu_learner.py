@@ -342,3 +342,12 @@ def test_fused_update_matches_torch_losses(recurrent, monkeypatch):
     assert set(g0) == set(g1)
     errs = {k: float((g0[k] - g1[k]).abs().max() / g1[k].abs().max().clamp_min(1e-8)) for k in g1}
     assert max(errs.values()) < 1e-3, errs
+
+
+def test_shipped_gemm_tuning_applies_on_this_box():
+    """The learner turns TunableOp on with the shipped per-shape results, and this image's validators (torch, HIP,
+    hipBLASLt, rocBLAS, gfx950) accept them: config D's recurrent product is among the loaded entries."""
+    from ouzelum_amd.learners.gemm_tuning import SHIPPED, enable_tuned_gemms
+    assert enable_tuned_gemms("cuda") and torch.cuda.tunable.is_enabled()
+    assert torch.cuda.tunable.read_file(SHIPPED)
+    assert any("tn_512_4096_128" in str(r) for r in torch.cuda.tunable.get_results())

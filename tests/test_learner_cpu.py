@@ -85,3 +85,13 @@ def test_learner_pomdp_oracle_modes():
     assert r.min() >= 0.75 - 1e-6 and r.max() <= 1.25 + 1e-6
     # sharded rows draw what the unsharded run draws for the same global rows
     np.testing.assert_array_equal(LO.pomdp_obs(x[100:], 2, 0.25, 11, 100, 0), y[100:])
+
+
+def test_gemm_tuning_is_gpu_only_and_can_be_turned_off(monkeypatch):
+    from ouzelum_amd.learners import gemm_tuning as G
+    assert not G.enable_tuned_gemms("cpu")
+    monkeypatch.setenv("OUZ_TUNABLEOP", "0")
+    assert not G.enable_tuned_gemms("cuda:0")
+    with open(G.SHIPPED) as fh:
+        head = fh.read()
+    assert "Validator,GCN_ARCH_NAME,gfx950" in head and "GemmTunableOp_float" in head
