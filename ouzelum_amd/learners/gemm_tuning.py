@@ -45,7 +45,7 @@ def enable_tuned_gemms(device):
         if os.path.exists(path):
             try:
                 T.read_file(path)
-            except RuntimeError as e:     # another build's file: TunableOp tunes those shapes instead
+            except Exception as e:        # another build's or a half-written file: those shapes are tuned instead
                 warnings.warn(f"TunableOp results {path} not used: {e}", stacklevel=2)
     _state["done"] = True
     return True
