@@ -56,6 +56,28 @@ torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
     agent.train(obs, pomdps, actions, next_obs, next_done, init, logprobs, rewards, dones)
     torch.cuda.synchronize()
+# the rollout too: wall time of 16 steps against the GPU time its kernels took
+import time  # noqa: E402
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as rprof:
+    rollout()
+    torch.cuda.synchronize()
+wall_profiled = time.perf_counter() - t0
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+rollout()
+torch.cuda.synchronize()
+wall = time.perf_counter() - t0
+gpu_us = sum(getattr(e, "self_device_time_total", 0) or 0 for e in rprof.key_averages()
+             if getattr(e, "device_type", None) is not None and "CUDA" in str(e.device_type))
+print(f"== rollout of {T} steps: wall {wall * 1e3:.3f} ms unprofiled, {wall_profiled * 1e3:.3f} ms profiled; "
+      f"GPU kernel time {gpu_us / 1e3:.3f} ms")
+rows_r = sorted(((e.key, e.count, getattr(e, "self_device_time_total", 0) or 0) for e in rprof.key_averages()),
+                key=lambda r: -r[2])
+for k, c, s_ in rows_r[:25]:
+    if s_ > 0:
+        print(f"{c:6d} {s_:10.1f} {k[:110]}")
 ka = prof.key_averages()
 rows = [(e.key, e.count, getattr(e, "self_device_time_total", 0) or getattr(e, "self_cuda_time_total", 0),
          getattr(e, "device_time_total", 0) or getattr(e, "cuda_time_total", 0)) for e in ka]
