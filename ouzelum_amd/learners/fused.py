@@ -189,6 +189,57 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=None):
+    """The T-step recurrence: per step the recurrent GEMM onto the input projection and one fused cell launch.
+    Returns (act, c_all, hid, hm, cm, keep).  ``carry_out=(h, c)``: the last step writes the final carry (keep = 1,
+    so the masked next-step carry is the carry itself) into these buffers instead of the scratch row; they may
+    alias h0 / c0, which are consumed (masked into hm[0] / cm[0]) before any cell launch."""
+    T, B, G4 = x_proj.shape
+    H = G4 // 4
+    dev = x_proj.device
+    stream = L.stream_ptr(dev)
+    x_proj = x_proj.contiguous()
+    keep = keep.contiguous().float()
+    act = torch.empty((T, B, G4), device=dev)
+    c_all = torch.empty((T, B, H), device=dev)
+    hid = torch.empty((T, B, H), device=dev)
+    hm = torch.empty((T + 1, B, H), device=dev)       # masked h entering each step (+1 scratch)
+    cm = torch.empty((T + 1, B, H), device=dev)       # masked c entering each step
+    torch.mul(h0, keep[0].unsqueeze(1), out=hm[0])
+    torch.mul(c0, keep[0].unsqueeze(1), out=cm[0])
+    inplace = _INPLACE_GATES
+    gates = None if inplace else torch.empty((B, G4), device=dev)
+    w_t = w_hh.t()
+    for t in range(T):
+        if inplace:
+            # the recurrent product accumulates onto the step's input projection in place (beta = 1, C = D):
+            # addmm with out= a separate buffer first copies the (B, 4H) projection into it, one runtime
+            # copy launch per step.  x_proj is the caller's own temporary (SplitKLinear / addmm output)
+            # and is not saved for the backward pass.
+            gates = x_proj[t]
+            torch.addmm(gates, hm[t], w_t, out=gates)
+        else:
+            torch.addmm(x_proj[t], hm[t], w_t, out=gates)
+        kn = keep[t + 1] if t + 1 < T else None
+        h_next, c_next = hm[t + 1], cm[t + 1]
+        if carry_out is not None and t == T - 1:
+            h_next, c_next = carry_out
+        L.check(L.lib.ouz_lstm_cell_fwd(gates.data_ptr(), cm[t].data_ptr(), _p(kn), act[t].data_ptr(),
+                                        c_all[t].data_ptr(), hid[t].data_ptr(), h_next.data_ptr(),
+                                        c_next.data_ptr(), B, H, stream), "ouz_lstm_cell_fwd")
+    return act, c_all, hid, hm, cm, keep
+
+
+def lstm_sequence_carry_inplace(x_proj, h0, c0, keep, w_hh, h_out, c_out):
+    """Inference form of ``LSTMSequence`` (no autograd): returns hid (T, B, H) and writes the final carry into
+    h_out / c_out (contiguous (B, H) buffers, which may be h0 / c0 themselves) instead of returning copies.  The
+    graphed rollout policy keeps its carry in its static input buffers this way: no copy in or out per step."""
+    for t, name in ((h_out, "h_out"), (c_out, "c_out")):
+        if not t.is_contiguous() or tuple(t.shape[-2:]) != (x_proj.shape[1], x_proj.shape[2] // 4):
+            raise ValueError(f"lstm_sequence_carry_inplace: {name} must be a contiguous (B, H) buffer")
+    return _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=(h_out, c_out))[2]
+
+
 class LSTMSequence(torch.autograd.Function):
     """(x_proj (T,B,4H), h0 (B,H), c0 (B,H), keep (T,B), W_hh (4H,H)) -> (hidden (T,B,H), h_T, c_T).
     keep[t] = 1 - done[t] zeroes the carry entering step t (model.py:42-46)."""
@@ -196,37 +247,9 @@ class LSTMSequence(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_proj, h0, c0, keep, w_hh):
         ctx.set_materialize_grads(False)     # unused h_T / c_T come back as None, not zero-filled tensors
-        T, B, G4 = x_proj.shape
-        H = G4 // 4
-        dev = x_proj.device
-        stream = L.stream_ptr(dev)
-        x_proj = x_proj.contiguous()
-        keep = keep.contiguous().float()
-        act = torch.empty((T, B, G4), device=dev)
-        c_all = torch.empty((T, B, H), device=dev)
-        hid = torch.empty((T, B, H), device=dev)
-        hm = torch.empty((T + 1, B, H), device=dev)       # masked h entering each step (+1 scratch)
-        cm = torch.empty((T + 1, B, H), device=dev)       # masked c entering each step
-        torch.mul(h0, keep[0].unsqueeze(1), out=hm[0])
-        torch.mul(c0, keep[0].unsqueeze(1), out=cm[0])
-        inplace = _INPLACE_GATES
-        gates = None if inplace else torch.empty((B, G4), device=dev)
-        w_t = w_hh.t()
-        for t in range(T):
-            if inplace:
-                # the recurrent product accumulates onto the step's input projection in place (beta = 1, C = D):
-                # addmm with out= a separate buffer first copies the (B, 4H) projection into it, one runtime
-                # copy launch per step.  x_proj is this function's own temporary (SplitKLinear / addmm output)
-                # and is not saved for the backward pass.
-                gates = x_proj[t]
-                torch.addmm(gates, hm[t], w_t, out=gates)
-            else:
-                torch.addmm(x_proj[t], hm[t], w_t, out=gates)
-            kn = keep[t + 1] if t + 1 < T else None
-            L.check(L.lib.ouz_lstm_cell_fwd(gates.data_ptr(), cm[t].data_ptr(), _p(kn), act[t].data_ptr(),
-                                            c_all[t].data_ptr(), hid[t].data_ptr(), hm[t + 1].data_ptr(),
-                                            cm[t + 1].data_ptr(), B, H, stream), "ouz_lstm_cell_fwd")
+        act, c_all, hid, hm, cm, keep = _lstm_forward(x_proj, h0, c0, keep, w_hh)
         ctx.save_for_backward(act, c_all, cm, hm, keep, w_hh)
+        T = hid.shape[0]
         return hid, hid[T - 1].clone(), c_all[T - 1].clone()
 
     @staticmethod

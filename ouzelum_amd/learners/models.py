@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 from torch.distributions.normal import Normal
 
-from .fused import LSTMSequence, SplitKLinear, linear, run_mlp
+from .fused import LSTMSequence, SplitKLinear, linear, lstm_sequence_carry_inplace, run_mlp
 
 
 def layer_init(layer, std=math.sqrt(2), bias_const=0.0):
@@ -79,6 +79,8 @@ class LSTMActor(nn.Module):
                 nn.init.orthogonal_(param, 1.0)
         self.actor_mean = layer_init(nn.Linear(hidden, n_act), std=0.01)
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
+        # (h, c) buffers of shape (1, B, H) that inference calls write their final carry into (GraphedPolicy)
+        self.carry_inplace = None
 
     def initial_state(self, num_envs, device):
         shape = (self.lstm.num_layers, num_envs, self.lstm.hidden_size)
@@ -97,6 +99,12 @@ class LSTMActor(nn.Module):
             x_proj = (SplitKLinear.apply(feats, self.lstm.weight_ih_l0, bias) if torch.is_grad_enabled()
                       else torch.addmm(bias, feats, self.lstm.weight_ih_l0.t()))
             keep = (1.0 - done).float().view(-1, B)
+            if self.carry_inplace is not None and not torch.is_grad_enabled():
+                # GraphedPolicy's static carry: the final (h, c) overwrite these buffers (no copies per step)
+                ho, co = self.carry_inplace
+                hid = lstm_sequence_carry_inplace(x_proj.view(-1, B, 4 * H), h[0], c[0], keep,
+                                                  self.lstm.weight_hh_l0, ho[0], co[0])
+                return hid.view(-1, H), (ho, co)
             hid, hT, cT = LSTMSequence.apply(x_proj.view(-1, B, 4 * H), h[0], c[0], keep, self.lstm.weight_hh_l0)
             return hid.view(-1, H), (hT.unsqueeze(0), cT.unsqueeze(0))
         x_proj = torch.addmm(bias, feats, self.lstm.weight_ih_l0.t())

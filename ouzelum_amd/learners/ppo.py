@@ -270,8 +270,9 @@ class GraphedPolicy:
     Inputs are copied into static buffers before each replay; the parameters are read in place
     (Adam updates them in place, so every replay sees the current policy).  The sample's standard
     normal draws are made by ``normal_`` into a static buffer before each replay (models._policy_head:
-    the sample is mean + std * eps).  The LSTM carry returned is the graph's output buffer and
-    is copied into the input buffer by the next call.
+    the sample is mean + std * eps).  The LSTM's final carry is written into the static carry input
+    buffers themselves (``LSTMActor.carry_inplace``), so a carry handed back from the previous replay
+    (``alias=True``) needs no copy; any other carry is copied in.
     """
 
     def __init__(self, learner, warmup=3):
@@ -287,15 +288,23 @@ class GraphedPolicy:
         self.s_eps = torch.zeros((state.shape[0], ln.actor.actor_logstd.shape[1]), device=ln.device)
         side = torch.cuda.Stream(device=ln.device)
         side.wait_stream(torch.cuda.current_stream(ln.device))
-        with torch.cuda.stream(side):   # warm-up: lazy workspaces / kernels resolved outside the capture
-            for _ in range(self.warmup):
-                ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
-        torch.cuda.current_stream(ln.device).wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        # relaxed: the caching allocator may map a fresh segment for the graph's private pool during
-        # the capture
-        with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
-            self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
+        # the LSTM's final carry is written back into the static input buffers (models.LSTMActor.carry_inplace),
+        # so the replay's output carry IS its next input: no copy in or out when the caller hands it back
+        if ln.recurrent and os.environ.get("OUZ_GRAPH_CARRY_INPLACE", "1") != "0":
+            ln.actor.carry_inplace = self.s_lstm
+        try:
+            with torch.cuda.stream(side):   # warm-up: lazy workspaces / kernels resolved outside the capture
+                for _ in range(self.warmup):
+                    ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
+            torch.cuda.current_stream(ln.device).wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            # relaxed: the caching allocator may map a fresh segment for the graph's private pool during
+            # the capture
+            with torch.cuda.graph(self.graph, capture_error_mode="relaxed"):
+                self.out = ln.get_action(self.s_in, self.s_lstm, self.s_done, eps=self.s_eps)
+        finally:
+            if ln.recurrent:
+                ln.actor.carry_inplace = None
 
     def _matches(self, state, lstm_state, done):
         """The call has the captured shapes, dtypes and device (a broadcastable but different batch would
@@ -318,8 +327,9 @@ class GraphedPolicy:
         self.s_done.copy_(done)
         self.s_eps.normal_()
         if self.s_lstm is not None:
-            self.s_lstm[0].copy_(lstm_state[0])
-            self.s_lstm[1].copy_(lstm_state[1])
+            for dst, src in zip(self.s_lstm, lstm_state):
+                if src is not dst:          # the previous replay's carry handed back (alias=True): already there
+                    dst.copy_(src)
         self.graph.replay()
         if alias:
             return self.out

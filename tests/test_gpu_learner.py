@@ -161,8 +161,8 @@ def test_fused_lstm_and_splitk_gradients_match_torch():
     assert max(errs.values()) < 2e-4, errs
 
 
-@pytest.mark.parametrize("recurrent", [True, False])
-def test_graphed_policy_matches_eager(recurrent, monkeypatch):
+@pytest.mark.parametrize("recurrent,alias", [(True, False), (False, False), (True, True)])
+def test_graphed_policy_matches_eager(recurrent, alias, monkeypatch):
     """PPOLearner.act (the rollout step's policy replayed from a hipGraph) against the eager policy
     over 20 replays with changing inputs, done resets and an in-place parameter update in between:
     the LSTM carry is bit-identical, the log-prob of the sampled action is the eager Normal's, and
@@ -188,7 +188,9 @@ def test_graphed_policy_matches_eager(recurrent, monkeypatch):
             with torch.no_grad():
                 for p in agent.actor.parameters():
                     p.add_(0.01 * torch.randn(p.shape, device=dev, generator=g))
-        action, logprob, entropy, lstm = agent.act(state, lstm, done)
+        action, logprob, entropy, lstm = agent.act(state, lstm, done, alias=alias)
+        if alias and recurrent:   # the carry handed back is the graph's own input buffer (no copies)
+            assert lstm[0] is agent._graphed.s_lstm[0] and lstm[1] is agent._graphed.s_lstm[1]
         with torch.no_grad():
             if recurrent:
                 hidden, want_lstm = agent.actor.get_states(state, ref_lstm, done)
