@@ -64,8 +64,8 @@ extern "C" {
                                3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots;
                                4: physical domain randomisation (ouz_dr_physical, OUZ_I_RAND_STEP), DR noise
                                   frequency (ouz_dr_noise.frequency);
-                               5: learner loss / trunk-backward kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss,
-                                  ouz_tanh_bwd_bias) */
+                               5: learner kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss, ouz_tanh_bwd_bias,
+                                  ouz_policy_sample) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -433,6 +433,13 @@ int ouz_ppo_value_loss(const float* values, const float* returns, int32_t n, dou
 #define OUZ_COLSUM_BLOCKS 1024
 int ouz_tanh_bwd_bias(const float* dy, const float* y, int32_t rows, int32_t cols, float* workspace, float* dz,
                       float* dbias, void* stream);
+
+/* The rollout policy's mean head and sample in one launch (RPO-LSTM/model.py:52-70, PPO/model.py:31-40 with
+ * action None): mean = hidden W^T + b, action = mean + exp(logstd) eps, logprob = -1/2 sum eps^2 - sum logstd -
+ * A log sqrt(2 pi), entropy = sum logstd + A (1/2 + log sqrt(2 pi)); A = OUZ_NUM_ACT.  hidden [B][H] (H a multiple
+ * of 4) and W [A][H] 16-byte aligned, b / logstd [A], eps / action [B][A], logprob / entropy [B]. */
+int ouz_policy_sample(const float* hidden, const float* w, const float* b, const float* logstd, const float* eps,
+                      int32_t B, int32_t H, float* action, float* logprob, float* entropy, void* stream);
 
 #ifdef __cplusplus
 }

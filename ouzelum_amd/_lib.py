@@ -145,6 +145,7 @@ SIGNATURES = {
     "ouz_ppo_policy_loss": (_I, [_P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P, _P]),
     "ouz_ppo_value_loss": (_I, [_P, _P, _I, _P, _P, _P, _P]),
     "ouz_tanh_bwd_bias": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
+    "ouz_policy_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
 }
 LOSS_WS_DOUBLES = 10 * 256      # OUZ_LOSS_WS_DOUBLES
 COLSUM_BLOCKS = 1024            # OUZ_COLSUM_BLOCKS

@@ -179,9 +179,10 @@ __global__ void __launch_bounds__(kLossThreads) policy_loss_kernel(
 #pragma clang fp contract(off)
   __shared__ double sh[kLossThreads / 64];
   float mu = 0.0f, den = 1.0f;
-  if (norm_adv) {   // (adv - adv.mean()) / (adv.std() + 1e-8), std unbiased; moments summed in block order
-    double s = 0.0, ss = 0.0;
-    for (int b = 0; b < kLossBlocks; ++b) { s += adv_part[2 * b]; ss += adv_part[2 * b + 1]; }
+  if (norm_adv) {   // (adv - adv.mean()) / (adv.std() + 1e-8), std unbiased; moments summed by block_sum's fixed tree
+    static_assert(kLossBlocks == kLossThreads, "one thread per partial block");
+    const double s = block_sum(adv_part[2 * threadIdx.x], sh);
+    const double ss = block_sum(adv_part[2 * threadIdx.x + 1], sh);
     const double m = s / n;
     const double var = (ss - s * m) / (double)(n - 1);
     mu = (float)m;
@@ -347,6 +348,56 @@ __global__ void __launch_bounds__(256) colsum_finish_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// The rollout policy's head and sample in one launch (RPO-LSTM/model.py:52-70 get_action_and_value with
+// action None; PPO/model.py:31-40): mean = h W^T + b (A = 4 actions), action = mean + exp(logstd) eps, and the
+// Normal log-prob / entropy summed over the actions in the form of models._sample_head:
+//   log-prob = -1/2 sum eps^2 - (sum logstd + A log sqrt(2 pi)),  entropy = sum logstd + A (1/2 + log sqrt(2 pi)).
+// Four threads per row, one per action (the row's hidden vector read once per wave: the four lanes share each
+// address); the log-prob's sum over actions is a shuffle across the four lanes.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) policy_sample_kernel(const float* __restrict__ hid, const float* __restrict__ w,
+                                                            const float* __restrict__ b,
+                                                            const float* __restrict__ logstd,
+                                                            const float* __restrict__ eps, int B, int H,
+                                                            float* __restrict__ action, float* __restrict__ logprob,
+                                                            float* __restrict__ entropy) {
+#pragma clang fp contract(off)
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int row = t >> 2, a = t & 3;
+  const bool live = row < B;
+  float dot = 0.0f;
+  if (live) {
+    const float4* hr = reinterpret_cast<const float4*>(hid + (size_t)row * H);
+    const float4* wr = reinterpret_cast<const float4*>(w + (size_t)a * H);
+    for (int k = 0; k < (H >> 2); ++k) {
+      const float4 hv = hr[k], wv = wr[k];
+      dot = fmaf(hv.x, wv.x, dot);
+      dot = fmaf(hv.y, wv.y, dot);
+      dot = fmaf(hv.z, wv.z, dot);
+      dot = fmaf(hv.w, wv.w, dot);
+    }
+  }
+  const float ls = logstd[a];
+  const float e = live ? eps[(size_t)row * OUZ_NUM_ACT + a] : 0.0f;
+  const float m = dot + b[a];
+  // -1/2 sum eps^2 over the row's four lanes (lanes 4j .. 4j+3 of the wave)
+  float q = e * e;
+  q += __shfl_xor(q, 1, 64);
+  q += __shfl_xor(q, 2, 64);
+  float lsum = ls;
+  lsum += __shfl_xor(lsum, 1, 64);
+  lsum += __shfl_xor(lsum, 2, 64);
+  const float kLogSqrt2Pi = 0.918938533204672742f;
+  const float c = lsum + (float)OUZ_NUM_ACT * kLogSqrt2Pi;
+  if (!live) return;
+  action[(size_t)row * OUZ_NUM_ACT + a] = m + expf(ls) * e;
+  if (a == 0) {
+    logprob[row] = -c + (-0.5f) * q;
+    entropy[row] = c + 0.5f * (float)OUZ_NUM_ACT;
+  }
+}
+
 inline int grid(int n, int b) { return (n + b - 1) / b; }
 
 int launch_status(const char* what) {
@@ -461,6 +512,18 @@ int ouz_tanh_bwd_bias(const float* dy, const float* y, int32_t rows, int32_t col
   hipLaunchKernelGGL(tanh_bwd_colsum_kernel, dim3(kColBlocks), dim3(256), 0, s, dy, y, dz, workspace, rows, cols);
   hipLaunchKernelGGL(colsum_finish_kernel, dim3(grid(cols, 16)), dim3(256), 0, s, workspace, cols, dbias);
   return launch_status("tanh_bwd_colsum_kernel");
+}
+
+int ouz_policy_sample(const float* hidden, const float* w, const float* b, const float* logstd, const float* eps,
+                      int32_t B, int32_t H, float* action, float* logprob, float* entropy, void* stream) {
+  if (B <= 0 || H <= 0 || H % 4 || H > 4096) return set_error(OUZ_ERR_INVALID, "ouz_policy_sample: B > 0, H a multiple of 4");
+  if (!hidden || !w || !b || !logstd || !eps || !action || !logprob || !entropy)
+    return set_error(OUZ_ERR_INVALID, "ouz_policy_sample: null buffer");
+  if (((reinterpret_cast<uintptr_t>(hidden) | reinterpret_cast<uintptr_t>(w)) & 15u))
+    return set_error(OUZ_ERR_INVALID, "ouz_policy_sample: hidden and w must be 16-byte aligned");
+  hipLaunchKernelGGL(policy_sample_kernel, dim3(grid(B * OUZ_NUM_ACT, 256)), dim3(256), 0, (hipStream_t)stream, hidden,
+                     w, b, logstd, eps, B, H, action, logprob, entropy);
+  return launch_status("policy_sample_kernel");
 }
 
 }  // extern "C"

@@ -24,6 +24,7 @@ from .. import _lib as L
 
 _INPLACE_GATES = os.environ.get("OUZ_LSTM_INPLACE_GATES", "1") != "0"
 _FUSED_TANH = os.environ.get("OUZ_FUSED_TANH", "1") != "0"
+_FUSED_SAMPLE = os.environ.get("OUZ_FUSED_SAMPLE", "1") != "0"
 
 
 def _splits(k, n_out_tiles):
@@ -183,6 +184,28 @@ class ValueLoss(torch.autograd.Function):
     def backward(ctx, g):
         (dv,) = ctx.saved_tensors
         return dv * g, None
+
+
+def policy_sample_ok(hidden, head):
+    return (_FUSED_SAMPLE and hidden.is_cuda and not torch.is_grad_enabled() and hidden.dim() == 2
+            and hidden.dtype == torch.float32 and hidden.shape[1] % 4 == 0 and head.out_features == L.NUM_ACT
+            and head.bias is not None)
+
+
+def policy_sample(hidden, head, logstd, eps):
+    """The rollout policy's mean head + sample in one HIP launch (``ouz_policy_sample``): (action, log-prob,
+    entropy) as ``models._sample_head(head(hidden), logstd, eps)``."""
+    B, H = hidden.shape
+    dev = hidden.device
+    h = hidden.contiguous()
+    w, b, ls, e = (t.detach().contiguous() for t in (head.weight, head.bias, logstd, eps))
+    action = torch.empty((B, L.NUM_ACT), device=dev)
+    logprob = torch.empty(B, device=dev)
+    entropy = torch.empty(B, device=dev)
+    L.check(L.lib.ouz_policy_sample(h.data_ptr(), w.data_ptr(), b.data_ptr(), ls.data_ptr(), e.data_ptr(), B, H,
+                                    action.data_ptr(), logprob.data_ptr(), entropy.data_ptr(), L.stream_ptr(dev)),
+            "ouz_policy_sample")
+    return action, logprob, entropy
 
 
 def _p(t):

@@ -23,7 +23,10 @@ import torch
 import torch.nn as nn
 from torch.distributions.normal import Normal
 
-from .fused import LSTMSequence, SplitKLinear, linear, lstm_sequence_carry_inplace, run_mlp
+from .fused import (LSTMSequence, SplitKLinear, linear, lstm_sequence_carry_inplace, policy_sample, policy_sample_ok,
+                    run_mlp)
+
+L_NUM_ACT = 4   # the action width ouz_policy_sample computes (OUZ_NUM_ACT)
 
 
 def layer_init(layer, std=math.sqrt(2), bias_const=0.0):
@@ -52,6 +55,14 @@ class MLPActor(nn.Module):
         self.actor_logstd = nn.Parameter(torch.zeros(1, n_act))
 
     def forward(self, state, action=None, eps=None):
+        head = self.actor_mean[-1]
+        if action is None and _SAMPLE_FORM == "direct":
+            hidden = run_mlp(self.actor_mean[:-1], state)
+            if policy_sample_ok(hidden, head):
+                e = torch.randn((hidden.shape[0], L_NUM_ACT), device=hidden.device) if eps is None else eps
+                return policy_sample(hidden, head, self.actor_logstd, e)
+            return _policy_head(torch.nn.functional.linear(hidden, head.weight, head.bias), self.actor_logstd,
+                                action, self.rpo_alpha, eps)
         mean = run_mlp(self.actor_mean, state)
         return _policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps)
 
@@ -126,6 +137,9 @@ class LSTMActor(nn.Module):
 
     def forward(self, state, lstm_state, done, action=None, eps=None):
         hidden, lstm_state = self.get_states(state, lstm_state, done)
+        if action is None and _SAMPLE_FORM == "direct" and policy_sample_ok(hidden, self.actor_mean):
+            e = torch.randn((hidden.shape[0], L_NUM_ACT), device=hidden.device) if eps is None else eps
+            return (*policy_sample(hidden, self.actor_mean, self.actor_logstd, e), lstm_state)
         mean = linear(hidden, self.actor_mean)
         return (*_policy_head(mean, self.actor_logstd, action, self.rpo_alpha, eps), lstm_state)
 

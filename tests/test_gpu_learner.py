@@ -353,3 +353,22 @@ def test_shipped_gemm_tuning_applies_on_this_box():
     assert enable_tuned_gemms("cuda") and torch.cuda.tunable.is_enabled()
     assert torch.cuda.tunable.read_file(SHIPPED)
     assert any("tn_512_4096_128" in str(r) for r in torch.cuda.tunable.get_results())
+
+
+@pytest.mark.parametrize("B,H", [(8192 + 3, 128), (1024, 256)])
+def test_policy_sample_kernel_matches_the_direct_form(B, H):
+    """ouz_policy_sample (mean head + sample + log-prob + entropy in one launch) against models._sample_head over
+    the torch head, same ε."""
+    from ouzelum_amd.learners.fused import policy_sample
+    from ouzelum_amd.learners.models import _sample_head
+    g = torch.Generator(device="cuda").manual_seed(B)
+    head = torch.nn.Linear(H, 4).cuda()
+    hidden = torch.randn(B, H, device="cuda", generator=g)
+    logstd = torch.randn(1, 4, device="cuda", generator=g) * 0.4
+    eps = torch.randn(B, 4, device="cuda", generator=g)
+    with torch.no_grad():
+        got = policy_sample(hidden, head, logstd, eps)
+        want = _sample_head(torch.nn.functional.linear(hidden, head.weight, head.bias), logstd, eps)
+    torch.testing.assert_close(got[0], want[0], rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(got[1], want[1], rtol=1e-5, atol=2e-6)
+    torch.testing.assert_close(got[2], want[2].contiguous(), rtol=1e-6, atol=1e-6)
