@@ -95,3 +95,21 @@ def test_gemm_tuning_is_gpu_only_and_can_be_turned_off(monkeypatch):
     with open(G.SHIPPED) as fh:
         head = fh.read()
     assert "Validator,GCN_ARCH_NAME,gfx950" in head and "GemmTunableOp_float" in head
+
+
+def test_direct_sample_head_equals_the_normal_form():
+    """models._sample_head (the rollout's sample on the (1, A) log-std terms) against torch's Normal: same action,
+    log-prob and entropy within f32 rounding."""
+    import torch
+    from torch.distributions.normal import Normal
+    from ouzelum_amd.learners.models import _sample_head
+    g = torch.Generator().manual_seed(3)
+    mean = torch.randn(4096, 4, generator=g)
+    logstd = torch.randn(1, 4, generator=g) * 0.5
+    eps = torch.randn(4096, 4, generator=g)
+    a, lp, ent = _sample_head(mean, logstd, eps)
+    std = torch.exp(logstd.expand_as(mean))
+    p = Normal(mean, std, validate_args=False)
+    torch.testing.assert_close(a, mean + std * eps, rtol=0, atol=1e-6)
+    torch.testing.assert_close(lp, p.log_prob(a).sum(1), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ent, p.entropy().sum(1), rtol=1e-6, atol=1e-6)
