@@ -8,10 +8,14 @@ update: 21.8-22.4 -> 20.0-20.8 ms (``profiles/r05/learn/tunableop_ab.txt``).
 
 ``gemm_tuned_gfx950.csv`` holds the results of a tuning run of ``scripts/bench_learner.py`` on config D
 (``scripts/r05_learn_tunable.sh``); TunableOp only uses it when its validators (torch, HIP, hipBLASLt, rocBLAS
-versions and the GPU arch) match this process.  Shapes it lacks (other env counts) are tuned at first use and
-written, with the shipped results, to a per-user cache file at exit.  ``OUZ_TUNABLEOP=0`` leaves TunableOp
-alone; a ``PYTORCH_TUNABLEOP_*`` setting in the environment means the user drives TunableOp and nothing is
-changed here.  TunableOp is process-wide: it applies to every GEMM of the process once a learner is built.
+versions and the GPU arch) match this process.  Shapes it lacks (other env counts, other minibatch sizes) take
+the library's own heuristic pick: no GEMM is timed online by default, so the solution a shape gets does not depend
+on a timing run and is the same on every run and every rank.  ``OUZ_TUNABLEOP_TUNE=1`` opts in to online tuning
+of the missing shapes; only then are results written (with the shipped ones) to a per-user cache file at exit,
+and that file is read back by later runs.  ``OUZ_TUNABLEOP=0`` leaves TunableOp alone; a ``PYTORCH_TUNABLEOP_*``
+setting in the environment means the user drives TunableOp and nothing is changed here.  TunableOp is
+process-wide: it applies to every GEMM of the process once a training learner is built (inference-only callers,
+``play.py``, build their learner with ``tuned_gemms=False``).
 """
 import os
 import tempfile
@@ -38,10 +42,12 @@ def enable_tuned_gemms(device):
         return T.is_enabled()
     if _state["done"]:
         return True
+    tune = os.environ.get("OUZ_TUNABLEOP_TUNE", "0") == "1"
     T.enable(True)
-    T.tuning_enable(os.environ.get("OUZ_TUNABLEOP_TUNE", "1") != "0")
+    T.tuning_enable(tune)
+    T.write_file_on_exit(tune)
     T.set_filename(cache_file(), insert_device_ordinal=True)
-    for path in (SHIPPED, T.get_filename()):
+    for path in ((SHIPPED, T.get_filename()) if tune else (SHIPPED,)):
         if os.path.exists(path):
             try:
                 T.read_file(path)

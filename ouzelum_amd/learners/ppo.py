@@ -91,7 +91,7 @@ def gae(rewards, values, dones, next_value, next_done, gamma=0.99, lam=0.95):
 
 class PPOLearner:
     def __init__(self, observation_space, action_space, num_envs, device, recurrent=True, rollout_steps=16,
-                 lr=0.0026, num_minibatches=2, update_epochs=4):
+                 lr=0.0026, num_minibatches=2, update_epochs=4, tuned_gemms=True):
         self.obs_dim = observation_space
         self.act_dim = action_space
         self.num_envs = num_envs
@@ -113,7 +113,8 @@ class PPOLearner:
         self.minibatch_size = self.batch_size // num_minibatches
         if recurrent and num_envs % num_minibatches:
             raise ValueError("num_envs must divide into the minibatches")   # agent.py:72
-        enable_tuned_gemms(self.device)       # per-shape GEMM solutions (gemm_tuning.py); OUZ_TUNABLEOP=0: off
+        if tuned_gemms:
+            enable_tuned_gemms(self.device)   # per-shape GEMM solutions (gemm_tuning.py); OUZ_TUNABLEOP=0: off
         self.actor = (LSTMActor(observation_space, action_space) if recurrent
                       else MLPActor(observation_space, action_space)).to(self.device)
         self.critic = Critic(observation_space).to(self.device)

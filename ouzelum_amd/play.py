@@ -75,7 +75,9 @@ def _actions_fn(task, env, checkpoint, device, algo="rpo_lstm"):
     from .learners import PPOLearner
     if algo not in ("rpo_lstm", "ppo"):
         raise ValueError(f"algo={algo!r}: rpo_lstm or ppo")
-    agent = PPOLearner(env.observation_space, env.action_space, env.num_envs, device, recurrent=algo == "rpo_lstm")
+    # inference only: no process-wide TunableOp (gemm_tuning.py) for the player's few GEMMs
+    agent = PPOLearner(env.observation_space, env.action_space, env.num_envs, device, recurrent=algo == "rpo_lstm",
+                       tuned_gemms=False)
     agent.load(str(checkpoint))
     if algo == "ppo":
         return lambda obs, done: agent.actor.actor_mean(obs).clamp(-1.0, 1.0)
@@ -125,7 +127,9 @@ def play(cfg, quiet=False):
     obs = env.reset()["obs"]
     done = torch.zeros(n, dtype=torch.bool, device=dev)
     steps = 0
+    before = 0.0          # games finished before the last step (the run stops at the step that reaches games_num)
     while True:
+        before = float(tot[0])
         obs_d, rew, reset, _ = env.step(policy(obs, done))
         obs = obs_d["obs"]
         done = reset.bool()
@@ -139,11 +143,14 @@ def play(cfg, quiet=False):
         steps += 1
         if steps % 256 == 0:
             log.flush()
-            if float(tot[0]) >= games_num:
-                break
+        # rl_games' BasePlayer.run checks games_played >= n_games after every step with a done env and stops at
+        # the step whose episodes reach it: the same episode set here (one host read per step, as its .item())
+        if float(tot[0]) >= games_num:
+            break
     log.flush()
     games, rsum, ssum = (float(x) for x in tot.cpu())
-    out = {"task": task, "num_envs": n, "steps": steps, "games": int(games), "av_reward": rsum / max(games, 1.0),
+    out = {"task": task, "num_envs": n, "steps": steps, "games": int(games), "games_before_last_step": int(before),
+           "av_reward": rsum / max(games, 1.0),
            "av_steps": ssum / max(games, 1.0), "landings": int(env.landings()), "episodes_logged": log.epi,
            "trajectories": traj_dir, "metrics": metrics_dir, "tag": log.tag}
     if not quiet:

@@ -351,6 +351,8 @@ def test_shipped_gemm_tuning_applies_on_this_box():
     hipBLASLt, rocBLAS, gfx950) accept them: config D's recurrent product is among the loaded entries."""
     from ouzelum_amd.learners.gemm_tuning import SHIPPED, enable_tuned_gemms
     assert enable_tuned_gemms("cuda") and torch.cuda.tunable.is_enabled()
+    # no online tuning unless OUZ_TUNABLEOP_TUNE=1 (ADVICE r05): shapes the file lacks take the library's pick
+    assert not torch.cuda.tunable.tuning_is_enabled()
     assert torch.cuda.tunable.read_file(SHIPPED)
     assert any("tn_512_4096_128" in str(r) for r in torch.cuda.tunable.get_results())
 

@@ -13,6 +13,8 @@
     ``test_gpu_baseline_sizes.test_minimum_slice_lee_4096_x_1000``;
   - config C's full episode, QuadTracking 4096 envs x 700 steps x seeds {0, 1, 2}, with the bounds of
     ``test_gpu_full_episode``, plus every step's storage row of done masks against the oracle.
+* The kernels above 65 536 envs against the float64 oracle directly, every step: the fused
+  estimator rollout's single-step twin and the step kernels of every task family.
 Reference loop being timed: ``train_vec.py:14-18``; the step: ``ekf_lee_landed.py:308-530``.
 """
 import numpy as np
@@ -67,6 +69,30 @@ def step_margin(env, o, actions, conv_time):
     return np.minimum(m, np.abs(o.p[:, 2] - zd))
 
 
+def assert_step_matches_oracle(tag, env, o, margin):
+    """One VecTask.step of ``env`` (already launched) against the f64 oracle ``o`` stepped from the same state with the
+    same actions (step_margin), with test_single_step_parity's tolerances (written there: p 2e-5, v 1e-4, w 1e-3,
+    q 2e-6, obs 1e-4, rew 1e-5, reset / time-out masks and progress exact), on every env that did not come within
+    1e-4 of one of the step's discrete decisions (``margin``; test_gpu_env.near_threshold adds the done lines).  At
+    least 99 % of the envs must be compared.  The direct oracle pin of the kernels above 65 536 envs (VERDICT r05
+    item 3): the step kernels' 256-lane blocks, the identity layout, the mixed curriculum's per-task launches."""
+    from tests.hip_helpers import oracle_snapshot, quat_canon
+    from tests.test_gpu_env import near_threshold
+    g, r = gpu_snapshot(env), oracle_snapshot(o)
+    ok = (margin >= 1e-4) & ~near_threshold(o)
+    assert ok.sum() >= 0.99 * o.n, f"{tag}: only {ok.sum()} of {o.n} envs away from a decision threshold"
+    assert_close(f"{tag} p", g["p"][ok], r["p"][ok], 2e-5, 2e-5)
+    assert_close(f"{tag} v", g["v"][ok], r["v"][ok], 1e-4, 1e-5)
+    assert_close(f"{tag} w", g["w"][ok], r["w"][ok], 1e-3, 1e-4)
+    assert_close(f"{tag} q", quat_canon(g["q"][ok]), quat_canon(r["q"][ok]), 2e-6, 0)
+    assert_close(f"{tag} obs", g["obs"][ok], r["obs"][ok], 1e-4, 1e-5)
+    assert_close(f"{tag} rew", g["rew"][ok], r["rew"][ok], 1e-5, 1e-5)
+    np.testing.assert_array_equal(g["reset"][ok], r["reset"][ok], err_msg=f"{tag} reset")
+    np.testing.assert_array_equal(g["timeouts"][ok], r["timeouts"][ok], err_msg=f"{tag} time_outs")
+    np.testing.assert_array_equal(g["progress"][ok], r["progress"][ok], err_msg=f"{tag} progress")
+    return 1
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("task", ["QuadTracking", "QuadMixed"])
 def test_large_n_fused_estimator_rollout_matches_single_steps(ouz, task):
@@ -82,7 +108,7 @@ def test_large_n_fused_estimator_rollout_matches_single_steps(ouz, task):
     g = torch.Generator(device="cuda").manual_seed(14)
     ring = (torch.rand((RING, n, 4), device="cuda", generator=g) * 2 - 1).contiguous()
     ring_np = ring.cpu().numpy().astype(np.float64)
-    total, flips, near_total = 0.0, 0, 0
+    total, flips, near_total, oracle_pinned = 0.0, 0, 0, 0
     for seg, (k_steps, drain) in enumerate(((16, True), (40, False), (1, True), (16, True))):
         # each segment starts both envs from the same state (a's): a rollout's worth of f32 code-generation
         # differences, never the accumulated drift of the whole test
@@ -93,10 +119,12 @@ def test_large_n_fused_estimator_rollout_matches_single_steps(ouz, task):
         rows = ([], [], [], [])
         margin = np.full(n, np.inf)
         for k in range(k_steps):
-            margin = np.minimum(margin, step_margin(b, o, ring_np[k % RING], conv))
+            m = step_margin(b, o, ring_np[k % RING], conv)   # o: the oracle stepped from b's state
+            margin = np.minimum(margin, m)
             b.step(ring[k % RING])
             for r, buf in zip(rows, (b.obs_buf, b.rew_buf, b.reset_buf, b.timeout_buf)):
                 r.append(buf.clone())
+            oracle_pinned += assert_step_matches_oracle(f"{task} step {k} of {k_steps}", b, o, m)
         want = b.episode_stats(drain=drain).clone()
         torch.cuda.synchronize()
         near = torch.as_tensor(margin < 1e-4, device="cuda")   # from that step on an env may take the other branch
@@ -129,8 +157,38 @@ def test_large_n_fused_estimator_rollout_matches_single_steps(ouz, task):
         near_total += nn
         total += float(got[1])
     assert total > 1000, f"too few episodes finished ({total}): the reset / statistics paths were barely run"
+    assert oracle_pinned == 73
     print(f"{task} {n} envs: {total:.0f} episodes over 73 fused steps; per segment summed: {near_total} envs near a "
           f"decision threshold, {flips} of them parted from their single-step twin")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("task", ["LeeLanded", "QuadFault", "Ouzelum", "QuadTracking", "QuadMixed"])
+def test_large_n_step_kernels_match_oracle(ouz, task):
+    """VecTask.step above 65 536 envs (256-lane blocks, the identity slot layout; QuadFault / Ouzelum through the
+    pipelined quad_step_pipe_kernel, QuadMixed through one launch per task of a shard whose offset is a multiple of
+    64 but not of the 1344-id chunk) pinned to the f64 oracle step by step: 24 steps from a common state each,
+    across resets (30-step episodes) and, for the estimator tasks, the end of a 10-step convergence window.
+    Reference step: ekf_lee_landed.py:308-530 (lee_landed.py, ouzelum.py for the others)."""
+    n = 70016 + 37
+    off = 64 * 5 if task == "QuadMixed" else 0
+    kw = dict(seed=41, task=task, num_envs=n, sim_device="cuda:0", max_episode_length=30, env_id_offset=off,
+              num_envs_total=off + n + 4096)
+    if task in ("QuadTracking", "QuadMixed"):
+        kw["convergence_time"] = 10
+    env = ouz.make(**kw)
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=41, max_episode_length=30,
+                                env_id_offset=off, num_envs_total=off + n + 4096,
+                                **({"convergence_time": 10} if "convergence_time" in kw else {})))
+    rs = np.random.RandomState(6)
+    resets = 0
+    for k in range(24):
+        a = rs.uniform(-1.0, 1.0, (n, 4)).astype(np.float32)
+        m = step_margin(env, o, a.astype(np.float64), 10)
+        env.step(torch.as_tensor(a, device="cuda"))
+        assert_step_matches_oracle(f"{task} {n} envs step {k}", env, o, m)
+        resets += int(o.reset_buf.sum())
+    assert resets > n // 2, "too few resets: the reset path was barely run"
 
 
 def _plans(env, ring, storage, ks):
@@ -290,17 +348,20 @@ def test_cls_large_layout_is_bitwise_the_identity_layout(ouz, task, monkeypatch)
     assert torch.equal(a.irows(0, L.I_COUNT), b.irows(0, L.I_COUNT))
 
 
-def test_mixed_split_matches_one_launch(ouz, monkeypatch):
+@pytest.mark.parametrize("off", [0, 64 * 5])
+def test_mixed_split_matches_one_launch(ouz, off, monkeypatch):
     """The mixed curriculum above 65 536 envs steps as one launch per task (StepArgs.mix_split: each task's kernel
     and register budget over its own 1344-id chunks): bitwise the one-launch kernel (OUZ_MIXED_SPLIT=0), state and
     outputs.  Its fused rollouts keep the one-launch kernel by default (bitwise); the opt-in split rollout
     (OUZ_MIXED_SPLIT_ROLLOUT=1) gives the QuadTracking chunks' fused rollout bitwise the one-launch fused kernel's
     on those envs and the LeeLanded / QuadFault chunks, streamed, bitwise the per-step launches (the one-launch
-    fused kernel differs from those within float tolerance only, checked by the large-N test above)."""
+    fused kernel differs from those within float tolerance only, checked by the large-N test above).  ``off``: a
+    shard whose offset is a multiple of 64 but not of the chunk (mixed_task_tile's partial first chunk),
+    n not a multiple of 64, more envs in the job than in the shard."""
     from ouzelum_amd import _lib as L
     n = 70016 + 37
     kw = dict(seed=31, task="QuadMixed", num_envs=n, sim_device="cuda:0", track_episodes=True,
-              convergence_time=10, max_episode_length=30)
+              convergence_time=10, max_episode_length=30, env_id_offset=off, num_envs_total=off + n + 4096)
     d = ouz.make(**kw)                                        # the defaults: split steps, one-launch rollouts
     monkeypatch.setenv("OUZ_MIXED_SPLIT_ROLLOUT", "1")
     a = ouz.make(**kw)                                        # split steps and split rollouts (opt-in)
@@ -337,14 +398,14 @@ def test_mixed_split_matches_one_launch(ouz, monkeypatch):
         assert torch.equal(x_one, x_def)
     assert torch.equal(d.fstate, one.fstate) and torch.equal(stats[1], stats[2])
     sts, stats = [sts[0], sts[1], sts[3]], [stats[0], stats[1], stats[3]]
-    chunk_task = (torch.arange(n, device="cuda") // L.MIXED_CHUNK) % 3     # 0 LeeLanded, 1 QuadTracking, 2 QuadFault
+    chunk_task = ((off + torch.arange(n, device="cuda")) // L.MIXED_CHUNK) % 3   # 0 LeeLanded, 1 QuadTracking, 2 QuadFault
     trk, rest = chunk_task == 1, chunk_task != 1
     for x_split, x_one, x_per in zip(*sts):
         assert torch.equal(x_split[:, trk], x_one[:, trk])                # fused against fused
         assert torch.equal(x_split[:, rest], x_per[:, rest])              # streamed against per-step
     for buf in ("fstate", "istate"):
         fs, fo, fp = getattr(a, buf), getattr(one, buf), getattr(per, buf)
-        tile_task = ((torch.arange(fs.shape[0], device="cuda") * L.TILE) // L.MIXED_CHUNK) % 3
+        tile_task = ((off + torch.arange(fs.shape[0], device="cuda") * L.TILE) // L.MIXED_CHUNK) % 3
         assert torch.equal(fs[tile_task == 1], fo[tile_task == 1]) and torch.equal(fs[tile_task != 1], fp[tile_task != 1])
     # the split rollout's statistics: ouz_episode_stats over every env after the steps.  Episodes finish in all
     # three tasks (max_episode_length 30, mostly time-outs); the count agrees with the one-launch fused rollout's and

@@ -97,6 +97,15 @@ def test_gemm_tuning_is_gpu_only_and_can_be_turned_off(monkeypatch):
     assert "Validator,GCN_ARCH_NAME,gfx950" in head and "GemmTunableOp_float" in head
 
 
+def test_play_builds_its_learner_without_tunableop():
+    """the inference-only player does not turn on process-wide TunableOp."""
+    import inspect
+    from ouzelum_amd import play as P
+    from ouzelum_amd.learners.ppo import PPOLearner
+    assert inspect.signature(PPOLearner).parameters["tuned_gemms"].default is True
+    assert "tuned_gemms=False" in inspect.getsource(P._actions_fn)
+
+
 def test_direct_sample_head_equals_the_normal_form():
     """models._sample_head (the rollout's sample on the (1, A) log-std terms) against torch's Normal: same action,
     log-prob and entropy within f32 rounding."""

@@ -27,6 +27,8 @@ def test_ekf_experiment_play_run_writes_the_task_outputs(tmp_path):
         P.main(args)   # not an override of the reference's command line
     out = P.main([a for a in args if "max_episode_length" not in a] + ["games_num=8"])
     assert out["games"] >= 8 and out["av_steps"] > 0 and out["tag"] == "flicker_0.3"
+    # rl_games' player stops at the step whose finished episodes reach games_num
+    assert out["games_before_last_step"] < 8
     files = sorted(os.listdir(traj))
     assert files and all(f.startswith("flicker_0.3_ep_") and f.endswith(".csv") for f in files)
     with open(traj / files[0]) as fh:
@@ -56,7 +58,7 @@ def test_rl_task_plays_a_learner_checkpoint(tmp_path, algo):
     agent.save(prefix)
     out = P.main(["task=QuadFault", "test=True", "num_envs=8", "sim_device=cpu", f"checkpoint={prefix}", f"algo={algo}",
                   "games_num=8", f"traj_dir={tmp_path}/t", f"metrics_dir={tmp_path}/m"])
-    assert out["games"] >= 8 and torch.isfinite(torch.tensor(out["av_reward"]))
+    assert out["games"] >= 8 > out["games_before_last_step"] and torch.isfinite(torch.tensor(out["av_reward"]))
 
 
 @pytest.mark.gpu
@@ -65,5 +67,5 @@ def test_ekf_experiment_play_run_on_the_gpu(tmp_path):
     out = P.main(["task=EKFLeeLanded", "num_envs=512", "test=True", "headless=True", "max_iterations=1000",
                   "+POMDP=flicker", "+pomdp_prob=0.0", "games_num=600", f"traj_dir={tmp_path}/t",
                   f"metrics_dir={tmp_path}/m"])
-    assert out["games"] >= 600 and out["av_steps"] > 0 and out["tag"] == "flicker_0"
+    assert out["games"] >= 600 > out["games_before_last_step"] and out["av_steps"] > 0 and out["tag"] == "flicker_0"
     assert os.listdir(tmp_path / "t") and (tmp_path / "m" / "flicker_0.txt").exists()
