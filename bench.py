@@ -272,49 +272,89 @@ def loaded_lib_sha16():
     return _LIB_SHA
 
 
-def load_traffic(kernel, task, n):
+def summary_alg_bytes_per_env_step(kernel, task, n, steps):
+    """Algorithmic bytes per env-step of the workload a PMC summary profiled: a fused rollout of ``steps``-step
+    launches (its per-launch state bytes spread over ITS OWN launch length), a streamed rollout's step launches, or
+    the step kernel."""
+    if kernel == "rollout" and streamed_rollout(task, n):
+        return streamed_rollout_bytes_per_env_step(task, RING)
+    if kernel == "rollout":
+        return rollout_bytes_per_env_step(task, steps)
+    return BYTES_PER_ENV_STEP[task] + EPISODE_TRACK_BYTES
+
+
+def price_summary(d, kernel, task, n):
+    """A committed PMC summary priced on its own terms: the algorithmic bytes of the launch it
+    profiled (``steps_per_launch`` of the summary), its PMC traffic against them, and the HBM fraction of those bytes
+    over the summary's rocprofv3 --stats average duration.  Everything here is recomputable from the summary JSON and
+    the kernel_stats CSV committed beside it (tests/test_bench_line.py does)."""
+    steps = int(d.get("steps_per_launch", 1))
+    b = summary_alg_bytes_per_env_step(kernel, task, n, steps)
+    alg = b * n * steps
+    out = {"steps_per_launch": steps, "alg_bytes_per_env_step": round(b, 3), "alg_bytes_per_launch": round(alg)}
+    t = d.get("traffic_bytes_per_launch")
+    if t:
+        out["traffic_alg_ratio"] = round(t / alg, 4)
+    us = d.get("rocprof_avg_us")
+    if us and not (kernel == "rollout" and streamed_rollout(task, n)):
+        out["frac_from_rocprof_avg"] = round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 5)
+    return out
+
+
+def load_traffic(kernel, task, n, steps=None):
     """HBM bytes per launch of this kernel at this size from a committed PMC summary of THIS library build
     (scripts/gpu_roofline_evidence.sh: FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, separate passes, and the
-    rocprofv3 --stats average duration of the same workload), or None.  Summaries of another build are reported
-    as stale, not used."""
+    rocprofv3 --stats average duration of the same workload), or None.  A fused rollout prefers the summary of the
+    launch length ``steps`` the timed region ran (the driver's 20 steps are one 20-step launch); without one it takes
+    a summary of another launch length and prices it with that launch's own bytes (price_summary), never mixing the
+    two.  Summaries of another build are reported as stale, not used."""
     import glob
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", f"pmc_*_{kernel}_{task}_{n}_summary.json"),
                             recursive=True))
     if not hits:
         return None
     sha = loaded_lib_sha16()
-    newest_other = None
+    fused = kernel == "rollout" and not streamed_rollout(task, n)
+    want = (steps or evidence_launch_steps(n)) if fused else None
+    newest_other, best = None, None
     for h in reversed(hits):
         with open(h) as fh:
             d = json.load(fh)
         if d.get("lib_sha16") != sha:
             newest_other = newest_other or os.path.relpath(h, ROOT)
             continue
-        t = d.get("traffic_bytes_per_launch")
-        if not t:
+        if not d.get("traffic_bytes_per_launch"):
             continue
-        steps = d.get("steps_per_launch", 1)
-        if kernel == "rollout" and not streamed_rollout(task, n) and steps != evidence_launch_steps(n):
-            continue   # a summary of another launch length prices another workload
-        raw = d.get("fetch_size_kb_raw")
-        out = {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / (n * steps), 2),
-               "read_bytes_per_env_step": round(d["read_bytes_corrected"] / (n * steps), 2),
-               "read_bytes_per_env_step_uncorrected": round(raw * 1024 / (n * steps), 2) if raw else None,
-               "write_bytes_per_env_step": round(d["write_bytes"] / (n * steps), 2),
-               "source": os.path.relpath(h, ROOT), "lib_sha16": sha}
-        if d.get("rocprof_avg_us"):
-            out["rocprof_kernel_us_per_launch"] = round(d["rocprof_avg_us"], 3)
-            committed = h[:-len("_summary.json")] + "_kernel_stats.csv"   # the --stats CSV copied beside it
-            out["rocprof_stats"] = os.path.relpath(committed, ROOT) if os.path.exists(committed) \
-                else d.get("rocprof_stats_csv")
-        return out
-    return {"bytes_per_launch": None, "stale": f"no summary of library {sha}; newest of another build: {newest_other}"}
+        exact = not fused or d.get("steps_per_launch", 1) == want
+        if best is None or (exact and not best[2]):
+            best = (h, d, exact)
+        if exact:
+            break
+    if best is None:
+        return {"bytes_per_launch": None, "stale": f"no summary of library {sha}; newest of another build: {newest_other}"}
+    h, d, exact = best
+    t = d["traffic_bytes_per_launch"]
+    steps_s = d.get("steps_per_launch", 1)
+    raw = d.get("fetch_size_kb_raw")
+    out = {"bytes_per_launch": round(t), "bytes_per_env_step": round(t / (n * steps_s), 2),
+           "read_bytes_per_env_step": round(d["read_bytes_corrected"] / (n * steps_s), 2),
+           "read_bytes_per_env_step_uncorrected": round(raw * 1024 / (n * steps_s), 2) if raw else None,
+           "write_bytes_per_env_step": round(d["write_bytes"] / (n * steps_s), 2),
+           "steps_per_launch": steps_s, "launch_matches_timed": exact,
+           "source": os.path.relpath(h, ROOT), "lib_sha16": sha, **{f"summary_{k}": v for k, v in
+                                                                   price_summary(d, kernel, task, n).items()}}
+    if d.get("rocprof_avg_us"):
+        out["rocprof_kernel_us_per_launch"] = round(d["rocprof_avg_us"], 3)
+        committed = h[:-len("_summary.json")] + "_kernel_stats.csv"   # the --stats CSV copied beside it
+        out["rocprof_stats"] = os.path.relpath(committed, ROOT) if os.path.exists(committed) \
+            else d.get("rocprof_stats_csv")
+    return out
 
 
 NOMINAL_CLOCK_GHZ = 2.4   # the in-kernel clock of an unloaded MI355X (s_memtime probes, profiles/r03/valu_issue.jsonl)
 
 
-def load_issue(kernel, task, n):
+def load_issue(kernel, task, n, steps=None):
     """The issue-bound view of this kernel at this size from a committed scripts/gpu_valu.sh summary of THIS
     library build (PMC passes of SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* / SQ_INSTS_VALU and f64 counts), or
     None.  For the kernels that are not HBM-bound: where their time goes instead.
@@ -325,13 +365,22 @@ def load_issue(kernel, task, n):
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "**", f"valu_*_{mode}_{task}_{n}_summary.json"),
                             recursive=True))
     sha = loaded_lib_sha16()
+    want = (steps or evidence_launch_steps(n)) if mode == "rollout" else None
+    ok = [None, None]   # [the timed launch length, the evidence's default launch length]
     for h in reversed(hits):
         with open(h) as fh:
             d = json.load(fh)
         if d.get("lib_sha16") != sha:
             continue
-        if mode == "rollout" and d.get("steps_per_launch", 16) != evidence_launch_steps(n):
-            continue   # another launch length
+        spl = d.get("steps_per_launch", 16)
+        if mode != "rollout" or spl == want:
+            ok[0] = ok[0] or (h, d)
+        elif spl == evidence_launch_steps(n):
+            ok[1] = ok[1] or (h, d)
+    for hit in ok:
+        if hit is None:
+            continue
+        h, d = hit
         lat = n <= LATENCY_REGIME_ENVS
         us = d["wave_cycles"] / (NOMINAL_CLOCK_GHZ * 1e3) if lat else d["kernel_cycles"] / (d["clock_ghz"] * 1e3)
         # latency regime: one wave per SIMD, bound by that wave's instruction chain ("valu-issue"); large N: by
@@ -341,7 +390,8 @@ def load_issue(kernel, task, n):
                 "issue_active_frac": d["issue_active_frac"], "wait_frac": d["wait_frac"],
                 "chip_valu_frac": d["chip_valu_frac"], "simd_frac": d["simd_frac"], "f64_share": d["f64_share"],
                 "valu_insts_per_wave_step": d["valu_insts_per_wave_step"], "wave_cycles": d["wave_cycles"],
-                "kernel_us_from_counters": round(us, 3), "source": os.path.relpath(h, ROOT)}
+                "kernel_us_from_counters": round(us, 3), "steps_per_launch": d.get("steps_per_launch", 1) if
+                mode == "rollout" else 1, "source": os.path.relpath(h, ROOT)}
     return None
 
 
@@ -379,15 +429,19 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1, region_step
     achieved = b * n / (us_per_step * 1e-6) / 1e9
     # a streamed rollout's launches are step kernels writing a storage row instead of the env buffers: priced with
     # the summary of that workload itself (scripts/gpu_roofline_evidence.sh rollout entries)
-    traffic = load_traffic(kernel, task, n)
+    timed_launch = launch_sizes(region_steps, steps_per_launch)[0] if region_steps else steps_per_launch
+    traffic = load_traffic(kernel, task, n, timed_launch if kernel == "rollout" else None)
     e = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
          "frac": round(achieved / HBM_PEAK_GBPS, 5),
          "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_detail": traffic,
          "kernel": "quad_rollout_kernel" if kernel == "rollout" and not streamed else step_kernel_name(task, n),
-         "steps_per_launch": 1 if streamed else steps_per_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
-         "bytes_per_launch": round(b * n * (1 if streamed else steps_per_launch)), "kernel_us": round(us_per_step, 3),
-         "kernel_us_per_launch": round(us_per_step * (1 if streamed else steps_per_launch), 3)}
-    issue = None if streamed else load_issue(kernel, task, n)
+         # the launches the priced region ran (a 20-step region of up-to-32-step launches: one 20-step launch)
+         "steps_per_launch": 1 if streamed else timed_launch, "num_envs": n, "bytes_per_env_step": round(b, 2),
+         "bytes_per_launch": round(b * n * (1 if streamed else timed_launch)), "kernel_us": round(us_per_step, 3),
+         "kernel_us_per_launch": round(us_per_step * (1 if streamed else timed_launch), 3)}
+    if kernel == "rollout" and not streamed and timed_launch != steps_per_launch:
+        e["launch_capacity"] = steps_per_launch
+    issue = None if streamed else load_issue(kernel, task, n, timed_launch if kernel == "rollout" else None)
     if issue:
         e["issue"] = issue
         if e["frac"] < 0.4:   # not HBM-bound: what binds it instead, from the counters
@@ -398,11 +452,13 @@ def roofline_entry(kernel, task, n, us_per_step, steps_per_launch=1, region_step
         e["frac_from_rocprof_avg"] = None
         e["rocprof_note"] = "step launches only (the rollout's copy and statistics launches are not in the summary)"
     elif traffic and traffic.get("rocprof_kernel_us_per_launch"):
-        # the same pricing from the committed rocprofv3 --stats average of this build (profiles/): the judge's
-        # reproduction of frac from a committed record
-        spl = 1 if streamed else steps_per_launch
-        us = traffic["rocprof_kernel_us_per_launch"] / spl
-        e["frac_from_rocprof_avg"] = round(b * n / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 5)
+        # the same pricing from the committed rocprofv3 --stats average of this build (profiles/), with the bytes of
+        # the launch that summary profiled (price_summary): the judge's reproduction of frac from committed records
+        e["frac_from_rocprof_avg"] = traffic.get("summary_frac_from_rocprof_avg")
+    if traffic and traffic.get("bytes_per_launch"):
+        # PMC traffic against the algorithmic bytes of the SAME launch (the summary's own launch length)
+        e["traffic_alg_ratio"] = traffic.get("summary_traffic_alg_ratio")
+        e["traffic_steps_per_launch"] = traffic["steps_per_launch"]
     if streamed:
         e["rollout"] = (f"streamed: {steps_per_launch} step launches per {steps_per_launch}-step rollout, straight "
                         "into the storage rows, then the statistics launch (the per-rollout copy and statistics "
@@ -702,7 +758,8 @@ def spawn_ranks(args):
 # ----------------------------------------------------------------------------------------- output
 LINE_LIMIT = 6000   # the stdout line stays well under what the driver parses (BENCH_r03's 26 KB line was not)
 _ROOF_KEYS = ("bound", "binding", "achieved", "peak", "unit", "frac", "traffic", "frac_from_rocprof_avg", "kernel",
-              "steps_per_launch", "num_envs", "bytes_per_env_step", "kernel_us", "kernel_us_back_to_back")
+              "steps_per_launch", "num_envs", "bytes_per_env_step", "kernel_us", "kernel_us_back_to_back",
+              "traffic_steps_per_launch", "traffic_alg_ratio")
 
 
 def compact_roofline(e):

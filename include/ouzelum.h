@@ -60,12 +60,13 @@
 extern "C" {
 #endif
 
-#define OUZ_ABI_VERSION 5   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
+#define OUZ_ABI_VERSION 6   /* 2: trigger-class state layout of the estimator tasks (ouz_state_slots);
                                3: 1344-id curriculum chunks of OUZ_TASK_MIXED with the class layout, ouz_env_slots;
                                4: physical domain randomisation (ouz_dr_physical, OUZ_I_RAND_STEP), DR noise
                                   frequency (ouz_dr_noise.frequency);
                                5: learner kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss, ouz_tanh_bwd_bias,
-                                  ouz_policy_sample) */
+                                  ouz_policy_sample);
+                               6: sim_params gravity domain randomisation (ouz_set_dr_gravity) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -347,6 +348,14 @@ int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr);
  * mass / inertia / motor constant scaling ~ U(dr_lo, dr_hi) at every reset; the other tasks: none).  dr == NULL or
  * every distribution 0: off.  Takes effect at the next launch. */
 int ouz_set_dr_physical(ouz_env* env, const ouz_dr_physical* dr);
+/* sim_params gravity DR (VecTask.apply_randomizations' "sim_params": {"gravity": ...}, vec_task.py:556-566,648-660 ->
+ * dr_utils.apply_random_samples :162-172).  The non-environment gate re-samples every `frequency` steps (<= 1: every
+ * step): at step t the sim's gravity is that of the epoch e = t - t % frequency, ONE draw for the whole sim (not per
+ * env) of generate_random_samples(params, 3, e) (the schedule at e; setup_only is not read, as in the reference's
+ * sim_params path) from the counter RNG, applied per axis to the nominal (0, 0, -9.81): nominal * sample (scaling)
+ * or nominal + sample (additive).  It enters the integrator only (the Lee controller's mg and the RL thrust scale are
+ * the tasks' own constants, as in the reference).  dr == NULL or distribution 0: nominal gravity. */
+int ouz_set_dr_gravity(ouz_env* env, const ouz_dr_param* dr, int32_t frequency);
 int64_t ouz_get_step(const ouz_env* env);
 int ouz_set_step(ouz_env* env, int64_t step);
 

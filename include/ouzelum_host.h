@@ -20,6 +20,7 @@
  *                             tasks/ekf_lee_landed.py:132-135,319-331,667-674
  *   ouz_host_set_dr_noise     VecTask DR noise  tasks/base/vec_task.py:576-646  ouz_set_dr_noise
  *   ouz_host_set_dr_physical  VecTask physical DR  vec_task.py:547-563,680-756   ouz_set_dr_physical
+ *   ouz_host_set_dr_gravity   sim_params gravity DR  vec_task.py:556-566,648-660  ouz_set_dr_gravity
  *   ouz_host_get/set_step     the step counter (sim_step_count)              ouz_get_step / ouz_set_step
  */
 #ifndef OUZELUM_HOST_H_
@@ -52,6 +53,7 @@ int ouz_host_episode_stats(ouz_host_env* env, double* out, int32_t drain);
 int ouz_host_set_trace(ouz_host_env* env, float* trace, uint32_t* resets, int32_t env_index, int32_t capacity);
 int ouz_host_set_dr_noise(ouz_host_env* env, int32_t target, const ouz_dr_noise* dr);
 int ouz_host_set_dr_physical(ouz_host_env* env, const ouz_dr_physical* dr);
+int ouz_host_set_dr_gravity(ouz_host_env* env, const ouz_dr_param* dr, int32_t frequency);
 int64_t ouz_host_get_step(const ouz_host_env* env);
 int ouz_host_set_step(ouz_host_env* env, int64_t step);
 

@@ -34,6 +34,7 @@ RNG_DR = 4
 RNG_FAULT = 5
 RNG_DRN_OBS = 6         # VecTask DR noise on observations
 RNG_DRN_ACT = 7         # ... on actions
+RNG_GRAV = 8            # sim_params.gravity DR (one whole-batch draw per epoch, env id BATCH_ENV)
 RNG_POMDP = 16          # + call-site id
 BATCH_ENV = 0xFFFFFFFF  # env id used for whole-batch draws (one coin per call)
 INIT_STEP = 0xFFFFFFFF  # step id used for draws made at env creation

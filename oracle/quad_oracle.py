@@ -463,7 +463,8 @@ def deck_contact(p, v, w, on, plat, plat_v):
     return p, v, w
 
 
-def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, wmax=MAX_ANGVEL, contact=None):
+def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, wmax=MAX_ANGVEL, contact=None,
+              gravity=None):
     """Semi-implicit Euler over ``substeps`` sub-steps on a lumped rigid body.
 
     f_b, tau_b: body-frame force (N) and torque (N m) at the COM (LOCAL_SPACE,
@@ -471,10 +472,11 @@ def integrate(p, q, v, w, f_b, tau_b, mass, inertia, dt=DT, substeps=SUBSTEPS, w
     world frame (Isaac root-state convention).  |w| is clamped to
     ``wmax`` (asset max_angular_velocity).  Orientation uses the exact
     exponential map of the world-frame angular velocity.  ``contact`` adds the landing
-    deck after each sub-step's position update (``deck_contact``).
+    deck after each sub-step's position update (``deck_contact``).  ``gravity``: the sim's gravity vector
+    (default (0, 0, -9.81); sim_params gravity DR, ``gravity_dr``).
     """
     h = dt / substeps
-    g = np.array([0.0, 0.0, -GRAVITY], dtype=p.dtype)
+    g = np.array([0.0, 0.0, -GRAVITY] if gravity is None else gravity, dtype=p.dtype)
     for _ in range(substeps):
         R = quat_to_matrix_wxyz(xyzw_to_wxyz(q))
         v = v + h * ((R @ f_b[..., None])[..., 0] / mass[:, None] + g)
@@ -642,6 +644,31 @@ def dr_scale(p, sample, nominal):
     return (nominal + sample) / nominal if p["operation"] == 0 else sample
 
 
+GRAVITY_NOMINAL = (0.0, 0.0, -GRAVITY)   # sim_params.gravity of every drone task (cfg/task/EKFLeeLanded.yaml:31)
+
+
+def gravity_dr(p, seed, step):
+    """sim_params gravity DR (vec_task.py:556-566,648-660 -> dr_utils.apply_random_samples :162-172).  The
+    non-environment gate re-randomizes when ``last_step - last_rand_step >= frequency``: at step t the sample of the
+    epoch e = t - t % frequency (frequency <= 1: every step), drawn ONCE for the whole sim (not per env) as
+    generate_random_samples(params, 3, e) -- three samples, schedule evaluated at e -- from the counter RNG
+    (words k of draw(seed, BATCH_ENV, e, RNG_GRAV, 0) and, the gaussian's Box-Muller partners, of sub-block 1).
+    gravity[k] = nominal[k] * sample[k] (scaling) or nominal[k] + sample[k] (additive), per axis: a scaling sample
+    leaves the zero x / y components at zero, exactly as the reference's.  ``p``: an ouz_dr_param-shaped dict plus
+    ``frequency``.  Returns the (3,) gravity vector, evaluated as the kernel does (f32 sample and value)."""
+    freq = int(p.get("frequency", 1))
+    ep = step - step % freq if freq > 1 else step
+    ids = np.array([rng.BATCH_ENV], np.int64)
+    u = rng.draw_u32(seed, ids, ep, rng.RNG_GRAV, 0)
+    u2 = rng.draw_u32(seed, ids, ep, rng.RNG_GRAV, 1)
+    out = np.empty(3)
+    for k in range(3):
+        s = np.float32(np.asarray(dr_sample(p, u[k], u2[k], ep)).reshape(-1)[0])
+        nom = np.float32(GRAVITY_NOMINAL[k])
+        out[k] = float(nom + s if p["operation"] == 0 else nom * s)
+    return out
+
+
 # ---------------------------------------------------------------------------
 # Task presets (SURVEY §8a; BASELINE.json configs)
 # ---------------------------------------------------------------------------
@@ -719,6 +746,7 @@ class EnvConfig:
     dr_phys: dict | None = None  # physical DR ({frequency, params: [mass, inertia, motor constant]}); None: task default
     dr_obs: dict | None = None   # VecTask DR noise on observations / actions (dr_noise_apply's p)
     dr_act: dict | None = None
+    dr_gravity: dict | None = None   # sim_params gravity DR (gravity_dr's p); None: (0, 0, -9.81)
 
 
 def env_task_ids(cfg: EnvConfig):
@@ -887,9 +915,10 @@ class OracleEnv:
             inertia = inertia.copy()
             inertia[:, 2] = INERTIA[2] * (1.0 + (self.dr[:, 1] - 1.0) * INERTIA[0] / INERTIA[2])
         deck_on = np.array([self.specs[tt].target_mode != TGT_GOAL for tt in self.task_ids])
+        grav = gravity_dr(cfg.dr_gravity, cfg.seed, t) if cfg.dr_gravity and cfg.dr_gravity["distribution"] else None
         self.p, self.q, self.v, self.w = integrate(self.p, self.q, self.v, self.w, f_b, tau_b,
                                                    mass.astype(dtype), inertia.astype(dtype), dt, cfg.substeps,
-                                                   contact=(deck_on, self.plat, self.plat_v))
+                                                   contact=(deck_on, self.plat, self.plat_v), gravity=grav)
 
         # ---- post_physics_step (ekf_lee_landed.py:620-685) ----
         self.progress += 1

@@ -25,7 +25,7 @@ class OuzelumError(RuntimeError):
 
 
 # --- constants mirrored from include/ouzelum.h (checked against the library in tests) ---
-ABI_VERSION = 5
+ABI_VERSION = 6
 LAYOUT_VERSION = 4  # the ABI version whose state-slot rules (include/ouzelum.h "State slots") the layout follows
 TASK_OUZELUM, TASK_LEE_LANDED, TASK_EKF_LEE_LANDED, TASK_TRACKING, TASK_FAULT, TASK_MIXED, TASK_LANDING = range(7)
 NUM_TASKS = 7
@@ -127,6 +127,7 @@ SIGNATURES = {
     "ouz_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
     "ouz_set_dr_physical": (_I, [_P, ctypes.POINTER(OuzDrPhysical)]),
+    "ouz_set_dr_gravity": (_I, [_P, ctypes.POINTER(OuzDrParam), _I]),
     "ouz_get_step": (_I64, [_P]),
     "ouz_set_step": (_I, [_P, _I64]),
     "ouz_lee_control": (_I, [_I, _P, _P, _P, _P, _I, _P]),
@@ -168,6 +169,7 @@ HOST_SIGNATURES = {
     "ouz_host_set_trace": (_I, [_P, _P, _P, _I, _I]),
     "ouz_host_set_dr_noise": (_I, [_P, _I, ctypes.POINTER(OuzDrNoise)]),
     "ouz_host_set_dr_physical": (_I, [_P, ctypes.POINTER(OuzDrPhysical)]),
+    "ouz_host_set_dr_gravity": (_I, [_P, ctypes.POINTER(OuzDrParam), _I]),
     "ouz_host_get_step": (_I64, [_P]),
     "ouz_host_set_step": (_I, [_P, _I64]),
 }

@@ -48,7 +48,7 @@ FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}", "-Wn
          # machine scheduler for instruction-level parallelism: at the 4096-env bench size a CU runs ONE wave,
          # whose step is a dependent instruction chain (~6.7 cycles per instruction against the 4-cycle issue
          # floor), so latency hiding inside the wave beats occupancy.  Measured against the default
-         # (scripts/exp/lib_ab.sh, one box): fused LeeLanded 2.08 -> 2.02 us per step, per-step kernel
+         # (scripts/archive/lib_ab.sh, one box): fused LeeLanded 2.08 -> 2.02 us per step, per-step kernel
          # 3.51 -> 3.38 us, the other configs within +-1 %, large-N HBM fractions unchanged.  The iterative-ilp
          # and max-memory-clause strategies measured 1-3 % slower on the fused B / C / D steps
          # (profiles/r02/sched_strategy_ab.txt).

@@ -23,6 +23,7 @@ enum RngStream : uint32_t {
   RNG_FAULT = 5,
   RNG_DRN_OBS = 6,  // VecTask DR noise on observations (vec_task.py:576-646)
   RNG_DRN_ACT = 7,  // ... on actions
+  RNG_GRAV = 8,     // sim_params.gravity DR (vec_task.py:648-660): one whole-batch draw per epoch, env BATCH_ENV
   RNG_POMDP = 16,  // + call site
 };
 constexpr uint32_t BATCH_ENV = 0xFFFFFFFFu;

@@ -10,6 +10,7 @@
 #ifdef OUZ_HOST
 #include "host_compat.h"
 #endif
+#include <cstddef>
 #include <cstdlib>
 #include "../../include/ouzelum.h"
 #include "quad_math.h"
@@ -375,6 +376,35 @@ OUZ_DEV float dr_scale(const ouz_dr_param& p, float sample, float nominal) {
   return p.operation == 0 ? (nominal + sample) / nominal : sample;
 }
 constexpr float kMotorConstant = 8.54858e-06f;   // assets/x500/model.sdf:523 (T = k_f w^2 per rotor)
+
+// sim_params gravity DR (include/ouzelum.h ouz_set_dr_gravity; vec_task.py:556-566,648-660, dr_utils.py:162-172):
+// kept in device memory right after the two VecTask noise entries (StepArgs.drn), on when drn_mask bit 2 is set.
+struct GravDr {
+  ouz_dr_param p;
+  int32_t frequency;
+  int32_t reserved;
+};
+struct DrNonEnv {            // the device block StepArgs.drn points at
+  ouz_dr_noise noise[2];     // [0] observations, [1] actions
+  GravDr grav;
+};
+static_assert(offsetof(DrNonEnv, grav) == 2 * sizeof(ouz_dr_noise), "StepArgs.drn + 2 is the gravity entry");
+OUZ_DEV const GravDr& grav_dr_of(const ouz_dr_noise* drn) { return *reinterpret_cast<const GravDr*>(drn + 2); }
+
+// The gravity of step `step`: the non-environment gate re-randomizes every `frequency` steps, so it is the sample of
+// the epoch e = step - step % frequency (schedule at e), one whole-sim draw of generate_random_samples(params, 3, e)
+// (words k of the BATCH_ENV draws of stream RNG_GRAV), applied per axis to the nominal (0, 0, -9.81) as
+// apply_random_samples does (nominal * sample or nominal + sample).  Wave-uniform.  oracle: quad_oracle.gravity_dr.
+OUZ_DEV V3 gravity_dr(const GravDr& g, uint64_t seed, uint32_t step) {
+  const uint32_t f = (uint32_t)g.frequency;
+  const uint32_t ep = f > 1u ? step - step % f : step;
+  seed = cold_seed(seed);
+  const U4 u = draw(seed, BATCH_ENV, ep, RNG_GRAV, 0u);
+  const U4 u2 = g.p.distribution == 1 ? draw(seed, BATCH_ENV, ep, RNG_GRAV, 1u) : U4{0u, 0u, 0u, 0u};
+  const float s0 = dr_sample(g.p, u.x, u2.x, ep), s1 = dr_sample(g.p, u.y, u2.y, ep), s2 = dr_sample(g.p, u.z, u2.z, ep);
+  const float nz = -kGravity;
+  return g.p.operation == 0 ? v3(0.0f + s0, 0.0f + s1, nz + s2) : v3(0.0f * s0, 0.0f * s1, nz * s2);
+}
 
 // Wave-tiled SoA (include/ouzelum.h OUZ_FIDX): a wave's fields are contiguous
 // 256-byte rows, field f at offset f*256 from the wave's tile base.  The tile base is
@@ -967,10 +997,13 @@ OUZ_DEV void env_core(const StepArgs& a, const StepCtx& sc, int i, uint32_t gid,
     if constexpr (CTRL == CTRL_RL) R0 = quat_to_mat(S.q);
     const DeckContact deck{TGT != TGT_GOAL, S.plat.x, S.plat.y, S.plat_v.x, S.plat_v.y};
     const float h = c.dt / (float)c.substeps;
+    // sim_params gravity (gym.set_sim_params after apply_randomizations, vec_task.py:648-660): nominal unless DR'd
+    const V3 grav = (a.drn_mask & 4) ? gravity_dr(grav_dr_of(a.drn), a.seed, sc.step) : v3(0.0f, 0.0f, -kGravity);
     if (c.substeps == 2)   // the configured sub-step count (EKFLeeLanded.yaml:29), unrolled
-      integrate_thrust_body<2>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck);
+      integrate_thrust_body<2>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck, grav);
     else
-      integrate_thrust_body<0>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck, c.substeps);
+      integrate_thrust_body<0>(S.p, S.q, S.v, S.w, R0, f_b.z, tau_b, inv_m, I, inv_I, h, c.wmax, deck, grav,
+                               c.substeps);
   }
 
   OUZ_STAMP(4, false);
@@ -1047,6 +1080,17 @@ inline const char* dr_physical_error(const ouz_dr_physical* p) {
     if (q.schedule != 0 && q.schedule_steps <= 0) return "a schedule needs schedule_steps > 0";
     if (q.distribution == 3 && !(q.range[0] > 0.0f && q.range[1] > 0.0f)) return "a loguniform range must be positive";
   }
+  return nullptr;
+}
+
+// nullptr if the sim_params gravity DR parameters are valid, else what is wrong with them
+inline const char* dr_gravity_error(const ouz_dr_param* p, int32_t frequency) {
+  if (frequency < 0) return "frequency must be >= 0";
+  if (p->distribution < 0 || p->distribution > 3 || p->operation < 0 || p->operation > 1 || p->schedule < 0 ||
+      p->schedule > 2)
+    return "bad distribution / operation / schedule";
+  if (p->distribution && p->schedule != 0 && p->schedule_steps <= 0) return "a schedule needs schedule_steps > 0";
+  if (p->distribution == 3 && !(p->range[0] > 0.0f && p->range[1] > 0.0f)) return "a loguniform range must be positive";
   return nullptr;
 }
 

@@ -33,7 +33,7 @@ struct ouz_host_env {
   int64_t step;
   int32_t threads;          // OpenMP threads of a step (0: the runtime's default)
   float2 wp_tab[204];       // waypoint tables (lemniscate | circle | square)
-  ouz_dr_noise drn[2];      // VecTask DR noise: [0] observations, [1] actions
+  DrNonEnv drn;             // VecTask DR noise ([0] observations, [1] actions) and sim_params gravity
   StepArgs a;
 };
 
@@ -157,10 +157,10 @@ int ouz_host_create(const ouz_config* cfg, ouz_host_env** out) {
   e->step = 0;
   e->threads = 0;
   build_waypoints(e->wp_tab);
-  memset(e->drn, 0, sizeof(e->drn));
+  memset(&e->drn, 0, sizeof(e->drn));
   fill_step_args(cfg, e->a);
   e->a.wp_tab = e->wp_tab;
-  e->a.drn = e->drn;
+  e->a.drn = e->drn.noise;
   *out = e;
   return OUZ_OK;
 }
@@ -258,10 +258,22 @@ int ouz_host_set_dr_noise(ouz_host_env* env, int32_t target, const ouz_dr_noise*
   if (dr && (dr->distribution < 0 || dr->distribution > 2 || dr->operation < 0 || dr->operation > 1 ||
              dr->schedule < 0 || dr->schedule > 2 || (dr->schedule && dr->schedule_steps <= 0) || dr->frequency < 0))
     return host_fail(OUZ_ERR_INVALID, "ouz_host_set_dr_noise: bad distribution / operation / schedule / frequency");
-  if (dr) env->drn[target] = *dr;
-  else memset(&env->drn[target], 0, sizeof(ouz_dr_noise));
-  const bool on = env->drn[target].distribution != 0;
+  if (dr) env->drn.noise[target] = *dr;
+  else memset(&env->drn.noise[target], 0, sizeof(ouz_dr_noise));
+  const bool on = env->drn.noise[target].distribution != 0;
   env->a.drn_mask = on ? (env->a.drn_mask | (1 << target)) : (env->a.drn_mask & ~(1 << target));
+  return OUZ_OK;
+}
+
+int ouz_host_set_dr_gravity(ouz_host_env* env, const ouz_dr_param* dr, int32_t frequency) {
+  if (!env) return host_fail(OUZ_ERR_INVALID, "ouz_host_set_dr_gravity: null env");
+  ouz_dr_param p{};
+  if (dr) p = *dr;
+  if (const char* bad = dr_gravity_error(&p, frequency))
+    return host_fail(OUZ_ERR_INVALID, std::string("ouz_host_set_dr_gravity: ") + bad);
+  env->drn.grav.p = p;
+  env->drn.grav.frequency = frequency;
+  env->a.drn_mask = p.distribution ? (env->a.drn_mask | 4) : (env->a.drn_mask & ~4);
   return OUZ_OK;
 }
 

@@ -1306,8 +1306,8 @@ struct ouz_env {
   int64_t step;
   float2* wp_tab;   // device waypoint tables
   double* stats_partials;    // [kStatsMaxBlocks][3] per-block partials of episode_stats_kernel
-  ouz_dr_noise* drn_dev;     // [2] DR noise params (read by the step kernel only when enabled)
-  ouz_dr_noise drn_host[2];
+  ouz_dr_noise* drn_dev;     // DrNonEnv: [2] DR noise params + sim_params gravity (read only when enabled)
+  DrNonEnv drn_host;
   uint32_t* stats_ticket;    // its last-block counter (returns to 0 after every launch)
   double* wave_partials;     // [tiles][3] per-wave partials of the fused rollout statistics
   uint32_t* wave_ticket;     // their last-wave counter (returns to 0 after every launch)
@@ -1455,7 +1455,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
                 "hipMalloc(stats)");
   if (r) { (void)hipFree(e->wp_tab); delete e; return r; }
   e->stats_ticket = reinterpret_cast<uint32_t*>(e->stats_partials + kStatsMaxBlocks * 3);
-  r = hip_check(hipMalloc(&e->drn_dev, 2 * sizeof(ouz_dr_noise)), "hipMalloc(dr noise)");
+  r = hip_check(hipMalloc(&e->drn_dev, sizeof(DrNonEnv)), "hipMalloc(dr noise)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   // one partial per wave of the rollout grid: four per tile under the quad-lane class layout
   const size_t n_waves = (size_t)OUZ_TILES(state_slots(cfg->task, cfg->num_envs)) * 4;
@@ -1466,7 +1466,7 @@ int ouz_create(const ouz_config* cfg, ouz_env** out) {
   r = hip_check(hipMemset(e->wave_ticket, 0, sizeof(uint32_t)), "hipMemset(wave ticket)");
   if (r) { (void)hipFree(e->wave_partials); (void)hipFree(e->drn_dev); (void)hipFree(e->stats_partials);
            (void)hipFree(e->wp_tab); delete e; return r; }
-  std::memset(e->drn_host, 0, sizeof(e->drn_host));
+  std::memset(&e->drn_host, 0, sizeof(e->drn_host));
   r = hip_check(hipMemset(e->stats_ticket, 0, sizeof(uint32_t)), "hipMemset(stats)");
   if (r) { (void)hipFree(e->stats_partials); (void)hipFree(e->wp_tab); delete e; return r; }
   StepArgs& a = e->args;
@@ -1977,6 +1977,18 @@ int ouz_set_trace(ouz_env* env, float* trace, uint32_t* resets, int32_t env_inde
   return OUZ_OK;
 }
 
+// The non-environment DR block (noise + gravity) to the device and the step's enable bits.  Synchronous: the
+// parameters are in place before the next launch.
+static int sync_dr_nonenv(ouz_env* env) {
+  int r = hip_check(hipMemcpy(env->drn_dev, &env->drn_host, sizeof(env->drn_host), hipMemcpyHostToDevice),
+                    "hipMemcpy(dr noise)");
+  if (r) return r;
+  env->args.drn = env->drn_dev;
+  env->args.drn_mask = (env->drn_host.noise[0].distribution ? 1 : 0) | (env->drn_host.noise[1].distribution ? 2 : 0) |
+                       (env->drn_host.grav.p.distribution ? 4 : 0);
+  return OUZ_OK;
+}
+
 int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr) {
   if (!env || target < 0 || target > 1) return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad env or target");
   ouz_dr_noise p{};
@@ -1984,13 +1996,18 @@ int ouz_set_dr_noise(ouz_env* env, int32_t target, const ouz_dr_noise* dr) {
   if (p.distribution < 0 || p.distribution > 2 || p.operation < 0 || p.operation > 1 || p.schedule < 0 ||
       p.schedule > 2 || (p.schedule && p.schedule_steps <= 0) || p.frequency < 0)
     return fail(OUZ_ERR_INVALID, "ouz_set_dr_noise: bad distribution / operation / schedule / frequency");
-  env->drn_host[target] = p;
-  int r = hip_check(hipMemcpy(env->drn_dev, env->drn_host, sizeof(env->drn_host), hipMemcpyHostToDevice),
-                    "hipMemcpy(dr noise)");
-  if (r) return r;
-  env->args.drn = env->drn_dev;
-  env->args.drn_mask = (env->drn_host[0].distribution ? 1 : 0) | (env->drn_host[1].distribution ? 2 : 0);
-  return OUZ_OK;
+  env->drn_host.noise[target] = p;
+  return sync_dr_nonenv(env);
+}
+
+int ouz_set_dr_gravity(ouz_env* env, const ouz_dr_param* dr, int32_t frequency) {
+  if (!env) return fail(OUZ_ERR_INVALID, "ouz_set_dr_gravity: null env");
+  ouz_dr_param p{};
+  if (dr) p = *dr;
+  if (const char* bad = dr_gravity_error(&p, frequency)) return fail(OUZ_ERR_INVALID, std::string("ouz_set_dr_gravity: ") + bad);
+  env->drn_host.grav.p = p;
+  env->drn_host.grav.frequency = frequency;
+  return sync_dr_nonenv(env);
 }
 
 int ouz_set_dr_physical(ouz_env* env, const ouz_dr_physical* dr) {

@@ -828,17 +828,19 @@ OUZ_HD void integrate(V3& p, Q4& q, V3& v, V3& w, V3 f_b, V3 tau_b, float inv_m,
 // (the oracle keeps the world-frame form); it needs R(q) once at entry (shared with the
 // controller), R(q)'s third column between sub-steps and R(q) once at exit for the world-frame w.
 // |w| = |w_b| (the clamp) and w = 0 <=> w_b = 0 (the deck) carry over unchanged.
-// NSUB > 0: that many sub-steps, unrolled; NSUB = 0: nsub sub-steps in a loop.
+// NSUB > 0: that many sub-steps, unrolled; NSUB = 0: nsub sub-steps in a loop.  g: the gravity vector.
 template <int NSUB>
 OUZ_HD void integrate_thrust_body(V3& p, Q4& q, V3& v, V3& w, const M3& R0, float fz, V3 tau_b, float inv_m, V3 I,
-                                  V3 inv_I, float h, float wmax, DeckContact deck, int nsub = NSUB) {
+                                  V3 inv_I, float h, float wmax, DeckContact deck, V3 g, int nsub = NSUB) {
   V3 wb = mtv(R0, w);
   V3 z = v3(R0.m[2], R0.m[5], R0.m[8]);
   const float acc = fz * inv_m;
   for (int s = 0; s < (NSUB > 0 ? NSUB : nsub); ++s) {   // a constant NSUB unrolls by itself
     if (s > 0)   // third column of R(q) for the unit quaternion q (normalised at the end of every sub-step)
       z = v3(2.0f * (q.x * q.z + q.y * q.w), 2.0f * (q.y * q.z - q.x * q.w), 1.0f - 2.0f * (q.x * q.x + q.y * q.y));
-    v = v + h * v3(z.x * acc, z.y * acc, z.z * acc - kGravity);
+    // g: the sim's gravity, (0, 0, -kGravity) unless sim_params DR'd (with g.x = g.y = 0 the x / y terms round as
+    // the plain products: a * b + 0 is the product)
+    v = v + h * v3(z.x * acc + g.x, z.y * acc + g.y, z.z * acc + g.z);
     const V3 c = cross(wb, mul(I, wb));
     wb = wb + h * mul(inv_I, tau_b - c);
     float n2 = dot(wb, wb);

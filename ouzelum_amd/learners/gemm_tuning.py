@@ -7,7 +7,7 @@ library default is not the fastest solution for the small ones: e.g. the recurre
 update: 21.8-22.4 -> 20.0-20.8 ms (``profiles/r05/learn/tunableop_ab.txt``).
 
 ``gemm_tuned_gfx950.csv`` holds the results of a tuning run of ``scripts/bench_learner.py`` on config D
-(``scripts/r05_learn_tunable.sh``); TunableOp only uses it when its validators (torch, HIP, hipBLASLt, rocBLAS
+(``scripts/archive/r05_learn_tunable.sh``); TunableOp only uses it when its validators (torch, HIP, hipBLASLt, rocBLAS
 versions and the GPU arch) match this process.  Shapes it lacks (other env counts, other minibatch sizes) take
 the library's own heuristic pick: no GEMM is timed online by default, so the solution a shape gets does not depend
 on a timing run and is the same on every run and every rank.  ``OUZ_TUNABLEOP_TUNE=1`` opts in to online tuning

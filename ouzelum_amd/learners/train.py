@@ -6,8 +6,11 @@ Same loop as the reference: T-step rollout with the LSTM carry reset on done, th
 actor acting on the clean observations and training on the learner-side POMDP ones
 (App. B item 10; ``--rollout_obs pomdp`` gives the RPO-LSTM_Critic variant), one
 PPO update per rollout, best/final checkpoints under the reference's file names.
-TensorBoard is not installed: the scalars of PPO/main.py:102-116 (average reward, episodic
-return / length) go to ``<logdir>/<run>.csv``.  Episode
+The reference's TensorBoard scalars (PPO/main.py:101-109: ``charts/episodic_return``, ``charts/episodic_length``,
+``average/average_reward``) go to a TensorBoard event file in ``<logdir>/<run>/`` (the reference's
+``SummaryWriter("../runs/<run>")``; written by ``tbevents.py``, tensorboard itself is not installed), one point per
+rollout: the mean return / length of the episodes that finished in it, where the reference logs the episodes that
+end in the rollout's first three steps one by one.  Every logged column also goes to ``<logdir>/<run>.csv``.  Episode
 statistics are the env's in-kernel [sum, count] (``ouz_episode_stats``), all-reduced
 over RCCL when launched with torchrun (one process per GPU, env ids sharded).
 """
@@ -23,6 +26,7 @@ import torch.distributed as dist
 from ..distributed import init_from_env, shard
 from ..vec_task import make
 from .ppo import PPOLearner
+from .tbevents import EventWriter
 from .wrappers import ExtractObsWrapper, POMDPWrapper, RecordEpisodeStatisticsTorch
 
 
@@ -71,9 +75,10 @@ def train(args):
     rewards = torch.zeros((T, N), device=device)
     dones = torch.zeros((T, N), device=device)
 
-    writer = None
+    writer = tb = None
     if rank == 0:
         os.makedirs(args.logdir, exist_ok=True)
+        tb = EventWriter(os.path.join(args.logdir, name))
         fh = open(os.path.join(args.logdir, name + ".csv"), "w", newline="")
         writer = csv.writer(fh)
         writer.writerow(["global_step", "average_reward", "episodes", "episodic_return", "episodic_length",
@@ -120,6 +125,11 @@ def train(args):
             writer.writerow([row[k] for k in ("global_step", "average_reward", "episodes", "episodic_return",
                                               "episodic_length", "pg_loss", "v_loss", "approx_kl", "clipfrac",
                                               "env_steps_per_s")])
+            if row["episodes"] > 0:
+                tb.add_scalar("charts/episodic_return", row["episodic_return"], global_step)
+                tb.add_scalar("charts/episodic_length", row["episodic_length"], global_step)
+            tb.add_scalar("average/average_reward", row["average_reward"], global_step)
+            tb.flush()
             if not args.quiet:
                 print(f"Step: {global_step}, Average rewards {row['average_reward']:.4f}, "
                       f"{sps / 1e6:.2f} M env-steps/s", flush=True)
@@ -131,8 +141,9 @@ def train(args):
         if not args.no_checkpoints:
             agent.save(os.path.join(args.checkpoint_dir, name))
         fh.close()
+        tb.close()
     elapsed = time.perf_counter() - t_start
-    return {"history": history, "agent": agent, "env": base, "elapsed": elapsed,
+    return {"history": history, "agent": agent, "env": base, "elapsed": elapsed, "events": tb.path if tb else None,
             "env_steps_per_s": global_step / elapsed}
 
 
@@ -145,7 +156,7 @@ def play(args):
                 track_episodes=True)
     env = ExtractObsWrapper(base)
     agent = PPOLearner(base.observation_space, base.action_space, N, device, recurrent=args.algo == "rpo_lstm",
-                       rollout_steps=args.rollout_steps)
+                       rollout_steps=args.rollout_steps, tuned_gemms=False)   # inference only
     if args.checkpoint:
         agent.load(args.checkpoint)
     next_obs = env.reset()

@@ -83,10 +83,9 @@ def parse_dr_params(dr_params):
     integer form: ``({"observations": noise | None, "actions": noise | None}, physical | None)``, where a noise
     entry is the ouz_dr_noise fields and ``physical`` is ``{"frequency", "params": [mass, inertia,
     motor_constant]}`` of ouz_dr_param fields (distribution 0: not randomized), or None without ``actor_params``
-    (the task default stays).  Raises NotImplementedError for what the build does not simulate."""
-    if "sim_params" in dr_params:
-        raise NotImplementedError("sim_params randomization (gravity, PhysX solver parameters) is not implemented: "
-                                  "the build's integrator has fixed gravity and no PhysX solver (DESIGN.md §3)")
+    (the task default stays).  Raises NotImplementedError for what the build does not simulate.  ``sim_params`` is
+    parsed by ``parse_sim_params``."""
+    parse_sim_params(dr_params)    # refuses what is not simulated before anything is set
     freq = int(dr_params.get("frequency", 1))   # vec_task.py:548
     if freq < 0:
         raise ValueError("frequency must be >= 0")
@@ -124,6 +123,39 @@ def parse_dr_params(dr_params):
                     raise ValueError(f"{DRONE_ACTOR}.{prop}.{attr}: a loguniform range must be positive")
                 params[k] = {**e, "setup_only": 1 if p.get("setup_only", False) else 0}
     return noise, {"frequency": freq, "params": params}
+
+
+def parse_sim_params(dr_params):
+    """dr_params["sim_params"] (vec_task.py:648-660) as the build's integer form: ``{"frequency", "param"}`` of the
+    gravity entry (ouz_dr_param fields; distribution 0: nominal gravity), or None without a ``sim_params`` entry.
+    ``gravity`` is the one sim parameter the build's integrator has (dr_utils.py:162-172); the PhysX solver parameters
+    (``rest_offset`` and the rest of gymapi.SimParams) raise NotImplementedError."""
+    sp = dr_params.get("sim_params")
+    if sp is None:
+        return None
+    freq = int(dr_params.get("frequency", 1))
+    if freq < 0:
+        raise ValueError("frequency must be >= 0")
+    off = {"distribution": 0, "operation": 0, "range": (0.0, 0.0), "schedule": 0, "schedule_steps": 0, "setup_only": 0}
+    for attr in sp or {}:
+        if attr != "gravity":
+            raise NotImplementedError(f"sim_params.{attr}: a PhysX solver parameter; the build's integrator has no PhysX "
+                                      "(DESIGN.md §3): only sim_params.gravity is randomizable")
+    p = (sp or {}).get("gravity")
+    if not p:
+        return {"frequency": freq, "param": off}
+    e = _dr_entry(p, "sim_params.gravity", _DR_DIST)
+    if e["distribution"] == 3 and not (e["range"][0] > 0 and e["range"][1] > 0):
+        raise ValueError("sim_params.gravity: a loguniform range must be positive")
+    return {"frequency": freq, "param": {**e, "setup_only": 0}}
+
+
+def _dr_param_struct(p):
+    q = L.OuzDrParam()
+    q.distribution, q.operation = p["distribution"], p["operation"]
+    q.range[0], q.range[1] = p["range"]
+    q.schedule, q.schedule_steps, q.setup_only = p["schedule"], p["schedule_steps"], p["setup_only"]
+    return q
 
 
 def _dr_noise_struct(p):
@@ -457,10 +489,29 @@ class QuadVecTask:
           setup_only}``, sampled at the lazy reset of every env whose randomize_buf >= frequency (:547-563).  An
           ``actor_params`` entry replaces the task's default physical DR (QuadTracking: mass / inertia / motor
           constant scaling ~ U(0.9, 1.1)); without one the default stays.
-        What this build does not simulate raises ``NotImplementedError``: ``sim_params`` (gravity, PhysX solver
-        parameters), other actors (the husky is kinematic, the marker visual), ``scale``, ``num_buckets``
-        (PhysX material buckets), other properties.  ``color`` is visual only and ignored."""
+        * ``sim_params.gravity`` (:648-660, dr_utils.py:162-172): one whole-sim sample of three values per
+          ``frequency`` steps (the non-environment gate), gravity = (0, 0, -9.81) * sample or + sample per axis,
+          into the integrator (``ouz_set_dr_gravity``).  Without a ``sim_params`` entry the gravity setting stays.
+        What this build does not simulate raises ``NotImplementedError``: the PhysX solver parameters of
+        ``sim_params``, other actors (the husky is kinematic, the marker visual), ``scale``, ``num_buckets``
+        (PhysX material buckets), other properties.  ``color`` is visual only and ignored.
+
+        Where the lumped body departs from the reference's per-body semantics (parity unpinned there):
+        Isaac Gym draws one sample per rigid body of the actor (vec_task.py:720-734; the x500 has five bodies), the
+        lumped body one per env; the reference treats ``inertia`` as a Mat33 for which dr_utils has no additive rule,
+        here additive inertia adds the one sample to each diagonal entry; ``motor_properties.motor_constant`` is not
+        in the reference's property getters (the SDF's motorConstant has no Isaac Gym setter) and is this build's
+        entry for the rotors' thrust constant.  tests/golden/dr_physical.npz pins the per-sample math
+        (generate_random_samples / apply_random_samples), not these mappings."""
         noise, phys = parse_dr_params(dr_params)
+        grav = parse_sim_params(dr_params)
+        if grav is not None:   # sim_params.gravity (vec_task.py:648-660); without a sim_params entry it stays as is
+            q = _dr_param_struct(grav["param"])
+            if self._host:
+                L.host_check(L.host_lib().ouz_host_set_dr_gravity(self._env, q, grav["frequency"]),
+                             "ouz_host_set_dr_gravity")
+            else:
+                L.check(L.lib.ouz_set_dr_gravity(self._env, q, grav["frequency"]), "ouz_set_dr_gravity")
         for target, key in ((0, "observations"), (1, "actions")):
             st = _dr_noise_struct(noise[key])
             if self._host:

@@ -1,5 +1,5 @@
 """Copy the rocprofv3 kernel stats and PMC summaries of one tagged GPU run from gpurun_out/
-into profiles/<tag>/ (tracked).   python scripts/collect_profiles.py r01"""
+into profiles/<tag>/ (tracked).   python scripts/archive/collect_profiles.py r01"""
 import glob
 import os
 import shutil

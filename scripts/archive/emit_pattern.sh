@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build and run scripts/exp/emit_pattern.hip on the GPU box: plain timing, a WRITE_SIZE pass and a
 # --kernel-trace --stats pass; summary JSON lines in gpurun_out/emit_pattern/summary.jsonl.
-#   bash scripts/exp/emit_pattern.sh [envs] [sleep]
+#   bash scripts/archive/emit_pattern.sh [envs] [sleep]
 set -eu
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=${1:-4096}; S=${2:-1}

@@ -3,7 +3,7 @@
 # (headline sizes, the large-N sweep, the streamed rollouts), the bench with the driver's arguments and with no
 # flags, and rocprofv3 --stats of the driver-argument command.  Every GPU step has its own time limit; the
 # script stops at the first failure.
-#   bash scripts/gpu_final_check.sh TAG
+#   bash scripts/archive/gpu_final_check.sh TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"

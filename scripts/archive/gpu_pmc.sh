@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic of the step kernel from PMC counters, one counter group per pass (MI355X_MICROARCH.md
 # §rocprofv3 PMC slots: FETCH_SIZE and WRITE_SIZE do not fit one pass).  Kernel trace only, no sys/hip trace.
-#   bash scripts/gpu_pmc.sh TAG TASK NUM_ENVS STEPS
+#   bash scripts/archive/gpu_pmc.sh TAG TASK NUM_ENVS STEPS
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; TASK=$2; N=$3; STEPS=${4:-200}

@@ -1,6 +1,6 @@
 """A/B of two library builds at large N (one child process per build and round, OUZ_LIB): the fused 16-step
 rollout (storage + statistics, bench.py's sweep entry) and the per-step kernel, GPU us per step back to back.
-    python scripts/exp/large_n_lib_ab.py A.so B.so [rounds] [task:envs ...]
+    python scripts/archive/large_n_lib_ab.py A.so B.so [rounds] [task:envs ...]
 """
 import json
 import os

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of a library variant on the large-N sweep entries (bench.sweep_entries: step kernel + fused / streamed
 # rollout, HIP events around back-to-back launches): product build and OUZ_LIB=$1 alternating twice.
-#   bash scripts/exp/large_n_lib_ab.sh VARIANT.so "QuadTracking QuadMixed" "4194304"
+#   bash scripts/archive/large_n_lib_ab.sh VARIANT.so "QuadTracking QuadMixed" "4194304"
 set -u
 cd "$(dirname "$0")/../.."
 V=$1; TASKS=$2; SIZES=$3

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of two in-tree library builds on the large-N step kernel: scripts/exp/pipe_ab.py under the product
-# library and under OUZ_LIB=$1, alternating twice.  Usage: bash scripts/exp/lib_ab.sh <variant.so> TASKS SIZES TILES
+# library and under OUZ_LIB=$1, alternating twice.  Usage: bash scripts/archive/lib_ab.sh <variant.so> TASKS SIZES TILES
 set -eu
 cd "$(dirname "$0")/../.."
 V=$1; T=$2; S=$3; P=${4:-1}

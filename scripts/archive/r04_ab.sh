@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 A/B batch: a library variant against the product build (scripts/exp/lib_ab.py), then the per-step
-# emit-pattern probe.   bash scripts/r04_ab.sh VARIANT.so TAG
+# emit-pattern probe.   bash scripts/archive/r04_ab.sh VARIANT.so TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 V=$1; TAG=$2

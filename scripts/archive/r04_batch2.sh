@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 batch: GPU suite on the in-tree library, A/B against a previous build (latency-regime configs and the
 # large-N estimator rollouts), the statistics-tail probe, the driver's bench command.
-#   bash scripts/r04_batch2.sh PREV.so TAG
+#   bash scripts/archive/r04_batch2.sh PREV.so TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 P=$1; TAG=$2
@@ -22,7 +22,7 @@ for k in sorted(agg):
     v = agg[k]
     print(k, "fused", sorted(x[0] for x in v), "step", sorted(x[1] for x in v), "sha", {x[2] for x in v}, {x[3] for x in v})
 PY
-timeout -k 10 900 bash scripts/exp/large_n_lib_ab.sh "$P" "QuadTracking QuadMixed EKFLeeLanded" "4194304" 2>&1 | grep -v amdgpu.ids > "$O/large_n_ab_$TAG.txt" || exit 1
+timeout -k 10 900 bash scripts/archive/large_n_lib_ab.sh "$P" "QuadTracking QuadMixed EKFLeeLanded" "4194304" 2>&1 | grep -v amdgpu.ids > "$O/large_n_ab_$TAG.txt" || exit 1
 grep rollout "$O/large_n_ab_$TAG.txt"
 timeout -k 10 300 python scripts/exp/stats_tail_probe.py 2>&1 | grep -v amdgpu.ids > "$O/stats_tail_$TAG.jsonl" || exit 1
 cat "$O/stats_tail_$TAG.jsonl"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU check of the in-tree library: GPU suite, smoke, the driver's bench command, counter list.
-#   bash scripts/r04_check.sh TAG
+#   bash scripts/archive/r04_check.sh TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r04}

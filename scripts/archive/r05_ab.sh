@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 A/B of the product library against a variant build (scripts/exp/lib_ab.py, 3 interleaved rounds).
-#   bash scripts/r05_ab.sh VARIANT.so TAG
+#   bash scripts/archive/r05_ab.sh VARIANT.so TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 V=$1; TAG=$2

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 batch 1 on one MI355X: (a) the driver's bench command with 16- against 32-step launches, interleaved;
 # (b) the learner update under rocprofv3 --kernel-trace --stats (config D, QuadFault 8192 envs).
-#   bash scripts/r05_batch1.sh
+#   bash scripts/archive/r05_batch1.sh
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O="$R/gpurun_out/r05b1"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-5 batch 2: A/B of the f64 EKF (product) against the round-4 f32 EKF (-DOUZ_EKF_F32), and of the statistics
-# hand-off with an agent-scope acquire (-DOUZ_STATS_ACQUIRE); then the GPU suite.   bash scripts/r05_batch2.sh
+# hand-off with an agent-scope acquire (-DOUZ_STATS_ACQUIRE); then the GPU suite.   bash scripts/archive/r05_batch2.sh
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O="$R/gpurun_out/r05b2"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5: learner GPU tests and the config D bench on the current library, then (same library) the headline
-# evidence part of scripts/gpu_evidence_r05.sh.   bash scripts/r05_learn_check.sh TAG
+# evidence part of scripts/gpu_evidence_r05.sh.   bash scripts/archive/r05_learn_check.sh TAG
 set -u
 TAG=$1
 O=gpurun_out/$TAG
@@ -15,5 +15,5 @@ for r in 1 2 3; do
     > $O/learn_$r.json 2> $O/learn_$r.err || { tail -5 $O/learn_$r.err; exit 1; }
   echo "round $r: $(cat $O/learn_$r.json)"
 done
-bash scripts/r05_learn_prof.sh $TAG > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+bash scripts/archive/r05_learn_prof.sh $TAG > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 bash scripts/gpu_evidence_r05.sh $TAG h

@@ -17,5 +17,5 @@ for r in 1 2 3; do
     echo "fused=$f round $r: $(cat $O/learn_f${f}_$r.json)"
   done
 done
-bash scripts/r05_learn_prof.sh r05o > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+bash scripts/archive/r05_learn_prof.sh r05o > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 tail -3 $O/prof.log

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The learner update under rocprofv3 --kernel-trace --stats (config D: QuadFault 8192 envs, RPO-LSTM; VERDICT r04
-# item 5).  Keeps the --stats summaries, drops the (large) per-dispatch trace.   bash scripts/r05_learn_prof.sh TAG
+# item 5).  Keeps the --stats summaries, drops the (large) per-dispatch trace.   bash scripts/archive/r05_learn_prof.sh TAG
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r05}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build and run scripts/exp/step_emit_pattern.hip on the GPU box: timing (both layouts interleaved), WRITE_SIZE and
 # FETCH_SIZE passes (separate runs); summary JSON lines in gpurun_out/step_emit_pattern/summary.jsonl.
-#   bash scripts/exp/step_emit_pattern.sh [envs] [sleep]
+#   bash scripts/archive/step_emit_pattern.sh [envs] [sleep]
 set -eu
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 N=${1:-4096}; S=${2:-2}

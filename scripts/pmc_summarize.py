@@ -5,8 +5,8 @@ gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the byt
 coalesced streaming reads -> doubled; WRITE_SIZE is exact for 16-B streaming stores.
 Writes profiles-ready JSON next to the raw counters:
     python pmc_summarize.py OUTDIR TAG TASK N            (round-1 layout: pmc_TAG_TASK_N_*, step kernel)
-    python pmc_summarize.py OUTDIR TAG TASK N MODE       (scripts/gpu_pmc2.sh / gpu_roofline_evidence.sh:
-                                                          pmc_TAG_MODE_TASK_N_*)
+    python pmc_summarize.py OUTDIR TAG TASK N MODE [K]   (scripts/gpu_pmc2.sh / gpu_roofline_evidence.sh:
+                                                          pmc_TAG_MODE_TASK_N_*; K: the rollout's launch length)
 A rollout of a task that streams it at this size (bench.py streamed_rollout) runs step kernels: its summary
 is the step kernel's.  ``lib_sha16``: the library the counters were taken on (bench.py only uses a summary of
 the library it loaded).
@@ -123,10 +123,10 @@ def main():
         fetch, nf = avg_counter(base + "_FETCH_SIZE/**/*counter_collection.csv", "FETCH_SIZE", kernel)
         write, nw = avg_counter(base + "_WRITE_SIZE/**/*counter_collection.csv", "WRITE_SIZE", kernel)
     steps = 1
-    if kernel == "quad_rollout_kernel<":   # kernel_driver.py's default launch length (bench.evidence_launch_steps)
+    if kernel == "quad_rollout_kernel<":   # kernel_driver.py's --launch-steps (default bench.evidence_launch_steps)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from bench import evidence_launch_steps
-        steps = evidence_launch_steps(n)
+        steps = int(sys.argv[6]) if len(sys.argv) > 6 else evidence_launch_steps(n)
     res = {"task": task, "num_envs": n, "kernel": kernel.rstrip("<"), "steps_per_launch": steps,
            "dispatches": [nf, nw], "fetch_size_kb_raw": fetch, "write_size_kb": write}
     try:

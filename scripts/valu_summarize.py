@@ -77,7 +77,7 @@ def main():
     if mode == "rollout":   # kernel_driver.py's default launch length (bench.evidence_launch_steps)
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         from bench import evidence_launch_steps
-        steps = evidence_launch_steps(n)
+        steps = int(sys.argv[6]) if len(sys.argv) > 6 else evidence_launch_steps(n)
     f64 = sum(c2[k] or 0.0 for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64",
                                      "SQ_INSTS_VALU_TRANS_F64"))
     res = {"task": task, "num_envs": n, "mode": mode, "kernel": kname.rstrip("<"), "steps_per_launch": steps,

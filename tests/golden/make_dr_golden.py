@@ -21,6 +21,12 @@ Writes tests/golden/dr_physical.npz: per case its parameters, step, parameter sl
 samples and the new property value of a nominal 1.0 ... the slot's nominal value (mass 2.064 kg, inertia xx 0.0293,
 motor constant 8.55e-6).  tests/test_dr_physical.py checks the oracle, the host build and (GPU) the HIP kernel
 against it.
+
+And tests/golden/dr_gravity.npz (round 6): the reference's ``apply_random_samples`` on a ``gymapi.SimParams`` stub
+whose ``gravity`` is a Vec3 (0, 0, -9.81) -- its sim_params gravity branch (dr_utils.py:160-172: three samples of
+generate_random_samples(params, 3, step), applied per axis) -- over every distribution x operation x schedule at the
+same steps, the draws being words k = 0..2 of the build's whole-sim gravity draws draw(seed, BATCH_ENV, step,
+RNG_GRAV, 0 / 1).  Per case: the parameters, step, the three samples and the new gravity vector.
 """
 import argparse
 import importlib.util
@@ -45,6 +51,12 @@ RANGES = {  # (distribution, operation) -> range
     ("uniform", "scaling"): (0.7, 1.3), ("uniform", "additive"): (-0.2, 0.3),
     ("loguniform", "scaling"): (0.5, 2.0), ("loguniform", "additive"): (0.01, 0.2),
     ("gaussian", "scaling"): (1.0, 0.15), ("gaussian", "additive"): (0.05, 0.1),
+}
+# sim_params gravity: a scaling sample multiplies (0, 0, -9.81) per axis, an additive one adds to it
+GRAVITY_RANGES = {
+    ("uniform", "scaling"): (0.8, 1.2), ("uniform", "additive"): (-0.5, 0.5),
+    ("loguniform", "scaling"): (0.7, 1.4), ("loguniform", "additive"): (0.05, 0.4),
+    ("gaussian", "scaling"): (1.0, 0.1), ("gaussian", "additive"): (0.0, 0.3),
 }
 SCHEDULES = (None, "linear", "constant")
 STEPS = (0, 30, 100, 250)
@@ -86,6 +98,59 @@ class CounterRandom:
 
 class Prop:   # a rigid-body property object (apply_random_samples' generic branch, dr_utils.py:193-204)
     pass
+
+
+class GravityRandom:
+    """np.random's uniform / normal over shape 3 as the build's whole-sim gravity draws at ``step``."""
+
+    def __init__(self, step):
+        ids = np.array([rng.BATCH_ENV], np.int64)
+        self.u = [w[0] for w in rng.draw_u32(SEED, ids, step, rng.RNG_GRAV, 0)][:3]
+        self.u2 = [w[0] for w in rng.draw_u32(SEED, ids, step, rng.RNG_GRAV, 1)][:3]
+
+    def uniform(self, lo, hi, shape):
+        assert shape == 3
+        return np.array([float(rng.uniform_f32(np.array([u]), float(np.float32(lo)), float(np.float32(hi)))[0])
+                         for u in self.u])
+
+    def normal(self, mu, var, shape):
+        assert shape == 3
+        return np.array([mu + var * float(Q._normal_from(np.array([a]), np.array([b]), False)[0])
+                         for a, b in zip(self.u, self.u2)])
+
+
+class Vec3:   # gymapi.Vec3's x / y / z
+    def __init__(self, x, y, z):
+        self.x, self.y, self.z = x, y, z
+
+
+def gravity_cases(du):
+    """The reference's sim_params gravity branch (dr_utils.py:160-172) on a SimParams stub."""
+    real_random = du.np.random
+    cases = []
+    for (dist, op), sched, step in itertools.product(GRAVITY_RANGES, SCHEDULES, STEPS):
+        params = {"range": list(GRAVITY_RANGES[(dist, op)]), "operation": op, "distribution": dist}
+        if sched:
+            params.update(schedule=sched, schedule_steps=SCHED_STEPS)
+        if dist == "loguniform" and op == "additive" and sched and step < SCHED_STEPS and \
+                (sched == "constant" or step == 0):
+            continue   # the scheduled range is 0 there: log(0) (not a usable case)
+        prop = du.gymapi.SimParams()
+        prop.gravity = Vec3(0.0, 0.0, -Q.GRAVITY)
+        og = {"gravity": Vec3(0.0, 0.0, -Q.GRAVITY)}
+        try:
+            du.np.random = GravityRandom(step)
+            s = du.generate_random_samples(dict(params), 3, step)
+            du.np.random = GravityRandom(step)
+            du.apply_random_samples(prop, og, "gravity", dict(params), step)
+        finally:
+            du.np.random = real_random
+        cases.append({"distribution": Q.DRP_DIST[dist], "operation": {"additive": 0, "scaling": 1}[op],
+                      "range": GRAVITY_RANGES[(dist, op)], "schedule": {None: 0, "linear": 1, "constant": 2}[sched],
+                      "schedule_steps": SCHED_STEPS if sched else 0, "step": step,
+                      "samples": [float(x) for x in np.asarray(s).reshape(-1)],
+                      "gravity": [prop.gravity.x, prop.gravity.y, prop.gravity.z]})
+    return cases
 
 
 def main():
@@ -132,6 +197,19 @@ def main():
         samples=np.array([c["samples"] for c in cases], np.float64),
         values=np.array([c["values"] for c in cases], np.float64))
     print(f"wrote {out}: {len(cases)} cases x {len(IDS)} envs")
+    g = gravity_cases(du)
+    out = os.path.join(HERE, "dr_gravity.npz")
+    np.savez_compressed(
+        out, seed=np.int64(SEED), nominal=np.array([0.0, 0.0, -Q.GRAVITY]),
+        distribution=np.array([c["distribution"] for c in g], np.int32),
+        operation=np.array([c["operation"] for c in g], np.int32),
+        range=np.array([c["range"] for c in g], np.float64),
+        schedule=np.array([c["schedule"] for c in g], np.int32),
+        schedule_steps=np.array([c["schedule_steps"] for c in g], np.int32),
+        step=np.array([c["step"] for c in g], np.int64),
+        samples=np.array([c["samples"] for c in g], np.float64),
+        gravity=np.array([c["gravity"] for c in g], np.float64))
+    print(f"wrote {out}: {len(g)} gravity cases")
 
 
 if __name__ == "__main__":

@@ -106,3 +106,73 @@ def test_launcher_reports_failed_rank():
                        text=True, timeout=300)
     assert p.returncode != 0
     assert '"metric"' not in p.stdout
+
+
+def _csv_avg_us(path, kernel):
+    """Average duration (us) of ``kernel`` in a committed rocprofv3 --stats kernel_stats.csv, read independently of
+    bench.py / pmc_summarize.py."""
+    import csv
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if row["Name"].startswith(kernel + "<"):
+                return float(row["AverageNs"]) / 1e3
+    return None
+
+
+def _committed_summaries(rnd="r06"):
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", rnd, "roofline", "pmc_*_summary.json")))
+
+
+def test_rocprof_priced_fraction_recomputes_from_committed_files():
+    """every committed PMC summary's rocprof-priced fraction is the algorithmic bytes of the
+    launch it profiled (its own steps_per_launch) over the kernel_stats CSV committed beside it, within 1 %; and its
+    PMC traffic is compared with the bytes of that same launch."""
+    hits = _committed_summaries()
+    if not hits:
+        pytest.skip("no round-6 evidence committed yet")
+    checked = 0
+    for h in hits:
+        with open(h) as fh:
+            d = json.load(fh)
+        if d.get("mixed_split") or not d.get("rocprof_avg_us"):
+            continue
+        task, n = d["task"], d["num_envs"]
+        kernel = "rollout" if d["kernel"] == "quad_rollout_kernel" else "step"
+        csv_path = h[:-len("_summary.json")] + "_kernel_stats.csv"
+        us = _csv_avg_us(csv_path, d["kernel"])
+        if kernel == "step" and us is None:
+            us = _csv_avg_us(csv_path, "quad_step_pipe_kernel")
+        assert us is not None, csv_path
+        steps = d["steps_per_launch"]
+        alg = (B.rollout_bytes_per_env_step(task, steps) if kernel == "rollout"
+               else B.BYTES_PER_ENV_STEP[task] + B.EPISODE_TRACK_BYTES) * n * steps
+        want = alg / (us * 1e-6) / 1e9 / B.HBM_PEAK_GBPS
+        if kernel == "rollout" and B.streamed_rollout(task, n):
+            continue
+        got = B.price_summary(d, kernel, task, n)
+        assert abs(got["frac_from_rocprof_avg"] - want) <= 0.01 * want, (h, got, want)
+        assert abs(got["traffic_alg_ratio"] - d["traffic_bytes_per_launch"] / alg) <= 1e-3, h
+        checked += 1
+    assert checked >= 4
+
+
+def test_headline_prices_the_driver_launch(monkeypatch):
+    """The driver's command (--steps 20: one 20-step launch) is priced with the 20-step launch's summary: its
+    traffic, rocprof average and algorithmic bytes all describe that launch."""
+    hits = [h for h in _committed_summaries() if "_rollout_LeeLanded_4096_" in h]
+    if not hits:
+        pytest.skip("no round-6 headline evidence committed yet")
+    with open(hits[-1]) as fh:
+        sha = json.load(fh)["lib_sha16"]
+    monkeypatch.setattr(B, "loaded_lib_sha16", lambda: sha)
+    e = B.roofline_entry("rollout", "LeeLanded", 4096, 1.8, B.MAX_LAUNCH_STEPS, 20)
+    assert e["steps_per_launch"] == 20 and e["traffic_steps_per_launch"] == 20, e
+    td = e["traffic_detail"]
+    assert td["launch_matches_timed"]
+    us = _csv_avg_us(os.path.join(ROOT, td["rocprof_stats"]), "quad_rollout_kernel")
+    want = B.rollout_bytes_per_env_step("LeeLanded", 20) * 4096 * 20 / (us * 1e-6) / 1e9 / B.HBM_PEAK_GBPS
+    assert abs(e["frac_from_rocprof_avg"] - want) <= 0.01 * want
+    assert abs(e["bytes_per_env_step"] - B.rollout_bytes_per_env_step("LeeLanded", 20)) < 0.01
+    assert e["traffic"] == td["bytes_per_launch"] and abs(e["traffic_alg_ratio"] - e["traffic"] / (
+        B.rollout_bytes_per_env_step("LeeLanded", 20) * 4096 * 20)) <= 1e-3

@@ -11,7 +11,10 @@ the lazy reset of every env whose randomize_buf >= F (:547-563) as dr_utils.gene
   the same per-env values -- f32 evaluation, so to 2e-6 relative (the gaussian's Box-Muller and the loguniform's
   exp / log in f32: 1e-5);
 * the frequency gate, setup_only and the motor-constant thrust scale against the oracle, step by step;
-* the schema's parsing, and what is refused.
+* the schema's parsing, and what is refused;
+* ``sim_params.gravity`` (vec_task.py:648-660, dr_utils.py:160-172; round 6): ``tests/golden/dr_gravity.npz`` holds
+  the reference's apply_random_samples on a SimParams gravity with the build's whole-sim draws; the oracle matches
+  it, and the host build / HIP kernel match the oracle step by step across the frequency gate's epochs.
 """
 import numpy as np
 import pytest
@@ -187,7 +190,7 @@ def test_schema_parsing_and_refusals():
     _, phys = parse_dr_params({"actor_params": {}})           # an empty actor_params turns physical DR off
     assert all(q["distribution"] == 0 for q in phys["params"])
     u = {"range": [0.5, 1.5], "operation": "scaling", "distribution": "uniform"}
-    for bad, exc in (({"sim_params": {"gravity": u}}, NotImplementedError),
+    for bad, exc in (({"sim_params": {"rest_offset": u}}, NotImplementedError),
                      ({"actor_params": {"husky": {"rigid_body_properties": {"mass": u}}}}, NotImplementedError),
                      ({"actor_params": {"Drone": {"scale": u}}}, NotImplementedError),
                      ({"actor_params": {"Drone": {"dof_properties": {"damping": u}}}}, NotImplementedError),
@@ -220,3 +223,115 @@ def test_quadtracking_default_is_the_schema_default():
     for _ in range(30):
         c.step(None)
     assert torch.all(c.frows(L.F_DR, L.F_DR + 3) == 1.0)
+
+
+# ------------------------------------------------------------------------------------------ sim_params gravity
+@pytest.fixture(scope="module")
+def gfx(golden):
+    return golden("dr_gravity.npz")
+
+
+def gravity_params(gfx, c, frequency=1):
+    p = {"range": [float(v) for v in gfx["range"][c]], "operation": ["additive", "scaling"][int(gfx["operation"][c])],
+         "distribution": DIST[int(gfx["distribution"][c])]}
+    if gfx["schedule"][c]:
+        p.update(schedule=["", "linear", "constant"][int(gfx["schedule"][c])],
+                 schedule_steps=int(gfx["schedule_steps"][c]))
+    return {"frequency": frequency, "sim_params": {"gravity": p}}
+
+
+def test_oracle_gravity_matches_reference_fixture(gfx):
+    """oracle.gravity_dr == the reference's apply_random_samples on SimParams.gravity (dr_utils.py:160-172) with the
+    build's whole-sim counter-RNG draws, every distribution x operation x schedule (f32 evaluation)."""
+    from ouzelum_amd.vec_task import parse_sim_params
+    for c in range(len(gfx["step"])):
+        g = parse_sim_params(gravity_params(gfx, c))
+        got = Q.gravity_dr({**g["param"], "frequency": 1}, int(gfx["seed"]), int(gfx["step"][c]))
+        t = 1e-5 if int(gfx["distribution"][c]) in (1, 3) else 2e-6
+        np.testing.assert_allclose(got, gfx["gravity"][c], rtol=t, atol=1e-6, err_msg=f"case {c}")
+        assert got[0] == gfx["gravity"][c][0] == 0.0 or int(gfx["operation"][c]) == 0   # scaling keeps x, y at 0
+
+
+GRAVITY_FREQ_CASES = [(1, 5), (4, 17), (9, 40)]   # (case index of the fixture, frequency)
+
+
+def run_gravity_case(device, gfx, c, freq, task="LeeLanded", steps=24):
+    """The env with sim_params gravity DR against the oracle step by step from identical states (the oracle loaded
+    with the env's state before each step): the gravity of each step's epoch enters the integrator, so the
+    post-step velocity pins it to dt * 1e-4 / 0.01 = 1e-2 m/s^2."""
+    n = 128
+    dr = gravity_params(gfx, c, freq)
+    env = ouzelum_amd.make(seed=int(gfx["seed"]), task=task, num_envs=n, sim_device=device, rl_device=device,
+                           max_episode_length=15)
+    env.apply_randomizations(dr)
+    from ouzelum_amd.vec_task import parse_sim_params
+    g = parse_sim_params(dr)
+    o = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_NAMES[task], num_envs=n, seed=int(gfx["seed"]), max_episode_length=15,
+                                dr_gravity={**g["param"], "frequency": g["frequency"]}))
+    rs = np.random.RandomState(2)
+    seen = set()
+    for k in range(steps):
+        a = rs.uniform(-1, 1, (n, 4)).astype(np.float32)
+        gpu_to_oracle(env, o)
+        o.step(a)
+        env.step(torch.as_tensor(a, device=device))
+        gs, r = gpu_snapshot(env), oracle_snapshot(o)
+        np.testing.assert_allclose(gs["v"], r["v"], rtol=1e-5, atol=1e-4, err_msg=f"step {k} v")
+        np.testing.assert_allclose(gs["p"], r["p"], rtol=2e-5, atol=2e-5, err_msg=f"step {k} p")
+        np.testing.assert_array_equal(gs["reset"], r["reset"], err_msg=f"step {k} reset")
+        seen.add(tuple(Q.gravity_dr({**g["param"], "frequency": freq}, int(gfx["seed"]), k)))
+    assert len(seen) == (steps + freq - 1) // freq, "one gravity per epoch of `frequency` steps"
+    # and it is not the nominal gravity: a gravity-free oracle parts from the env by dt * |g - g0| per step
+    return env
+
+
+@pytest.mark.parametrize("c,freq", GRAVITY_FREQ_CASES)
+def test_host_gravity_dr_against_oracle(gfx, c, freq):
+    run_gravity_case("cpu", gfx, c, freq)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,freq", GRAVITY_FREQ_CASES)
+def test_hip_gravity_dr_against_oracle(gfx, c, freq):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a HIP device")
+    run_gravity_case("cuda:0", gfx, c, freq)
+    run_gravity_case("cuda:0", gfx, c, freq, task="QuadTracking")   # the estimator kernels' integrator too
+
+
+def test_gravity_dr_moves_the_drone():
+    """A scaling sample of the gravity changes the free fall: with gravity DR the host env parts from the nominal
+    oracle by about dt * |g - g0| in v after one step, and matches the DR'd oracle."""
+    n = 64
+    dr = {"sim_params": {"gravity": {"range": [1.5, 1.5], "operation": "scaling", "distribution": "uniform"}}}
+    env = ouzelum_amd.make(seed=1, task="Ouzelum", num_envs=n, sim_device="cpu")
+    env.apply_randomizations(dr)
+    o0 = Q.OracleEnv(Q.EnvConfig(task=Q.TASK_OUZELUM, num_envs=n, seed=1))
+    gpu_to_oracle(env, o0)
+    a = np.zeros((n, 4), np.float32)
+    o0.step(a)
+    env.step(torch.as_tensor(a))
+    dv = gpu_snapshot(env)["v"][:, 2] - o0.v[:, 2]
+    np.testing.assert_allclose(dv, -0.5 * Q.GRAVITY * 0.01, rtol=1e-3)     # g_z = 1.5 * -9.81
+    env.apply_randomizations({"sim_params": {}})                            # an empty entry: nominal gravity again
+    gpu_to_oracle(env, o0)
+    o0.step(a)
+    env.step(torch.as_tensor(a))
+    np.testing.assert_allclose(gpu_snapshot(env)["v"], o0.v, atol=1e-4)
+
+
+def test_sim_params_parsing_and_refusals():
+    from ouzelum_amd.vec_task import parse_sim_params
+    u = {"range": [0.9, 1.1], "operation": "scaling", "distribution": "uniform"}
+    assert parse_sim_params({}) is None
+    g = parse_sim_params({"frequency": 30, "sim_params": {"gravity": u}})
+    assert g["frequency"] == 30 and g["param"]["distribution"] == 2 and g["param"]["operation"] == 1
+    assert parse_sim_params({"sim_params": {}})["param"]["distribution"] == 0
+    for bad, exc in (({"sim_params": {"rest_offset": u}}, NotImplementedError),
+                     ({"sim_params": {"gravity": {**u, "distribution": "beta"}}}, ValueError),
+                     ({"sim_params": {"gravity": {**u, "distribution": "loguniform", "range": [-1.0, 1.0]}}},
+                      ValueError)):
+        with pytest.raises(exc):
+            parse_sim_params(bad)
+        with pytest.raises(exc):
+            parse_dr_params(bad)      # the whole dr_params refuses it before anything is set

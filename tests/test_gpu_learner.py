@@ -86,6 +86,15 @@ def test_training_loop_runs(tmp_path, algo, env, n):
             assert np.isfinite(row[k]), (k, row)
     name = ("RPO_LSTM" if algo == "rpo_lstm" else "PPO") + "_flicker_0.1"
     assert (tmp_path / "runs" / f"{name}.csv").exists()
+    # the reference's SummaryWriter("../runs/<run>") scalars (PPO/main.py:101-109), one point per rollout
+    from ouzelum_amd.learners.tbevents import read_scalars
+    assert os.path.dirname(out["events"]) == str(tmp_path / "runs" / name)
+    pts, version = read_scalars(out["events"])
+    assert version == "brain.Event:2"
+    avg = [(s, v) for t, s, v, _ in pts if t == "average/average_reward"]
+    assert [s for s, _ in avg] == [r["global_step"] for r in h]
+    np.testing.assert_allclose([v for _, v in avg], [r["average_reward"] for r in h], rtol=1e-6)
+    assert {t for t, *_ in pts} <= {"charts/episodic_return", "charts/episodic_length", "average/average_reward"}
     assert (tmp_path / "ck" / f"{name}_actor").exists()
     # checkpoint round trip (agent.py:127-139), tensors only
     agent = out["agent"]
