@@ -44,8 +44,7 @@ def enable_tuned_gemms(device):
         return True
     tune = os.environ.get("OUZ_TUNABLEOP_TUNE", "0") == "1"
     T.enable(True)
-    T.tuning_enable(tune)
-    T.write_file_on_exit(tune)
+    T.tuning_enable(tune)   # TunableOp writes its results file at exit only while tuning is enabled
     T.set_filename(cache_file(), insert_device_ordinal=True)
     for path in ((SHIPPED, T.get_filename()) if tune else (SHIPPED,)):
         if os.path.exists(path):
