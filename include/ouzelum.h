@@ -66,7 +66,8 @@ extern "C" {
                                   frequency (ouz_dr_noise.frequency);
                                5: learner kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss, ouz_tanh_bwd_bias,
                                   ouz_policy_sample);
-                               6: sim_params gravity domain randomisation (ouz_set_dr_gravity) */
+                               6: sim_params gravity domain randomisation (ouz_set_dr_gravity), the fused LSTM
+                                  sequence kernels (ouz_lstm_seq_fwd / ouz_lstm_seq_bwd) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -413,6 +414,27 @@ int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* ke
 int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, const float* dhid, const float* G,
                       const float* dc_next, const float* keep_next, float* dgates, float* dc_prev, int32_t B, int32_t H,
                       void* stream);
+
+/* The whole LSTM recurrence of a (T, B) sequence in one launch each way, hidden size H = 128 (the reference actor's
+ * LSTM(256, 128), RPO-LSTM/model.py:34-50): the per-step GEMM + ouz_lstm_cell_fwd / _bwd pairs fused, the carry kept
+ * on chip, the recurrent product on the f32 MFMA.  Forward: x_proj [T][B][4H] (x W_ih^T + b_ih + b_hh), h0 / c0
+ * [B][H], keep [T][B] (1 - done before step t), w_hh the packed W_hh (w_fwd of ouz_lstm_seq_pack); writes hid
+ * [T][B][H] and, when not
+ * null, act [T][B][4H], c_all [T][B][H], hm / cm [T + 1][B][H] (the masked carry entering each step; row T the final
+ * carry unless h_out / c_out [B][H] take it, which may alias h0 / c0).  Backward: the saved act / c_all / cm, keep,
+ * the packed W_hh^T (w_bwd of ouz_lstm_seq_pack), dhid [T][B][H], dhT / dcT [B][H] or null; writes dgates
+ * [T][B][4H] and, when not null, dh0 = (dgates_0 W_hh) keep_0 and dc0 [B][H].  Same arithmetic per element as the
+ * per-step kernels; the products sum in another order (f32, within rounding of the GEMM path). */
+/* ouz_lstm_seq_pack: W_hh [4H][H] into the two fragment layouts the sequence kernels read (w_fwd, w_bwd: 4H * H
+ * floats each, 16-byte aligned; one contiguous 1 KB per wave per load), after every change of W_hh.  The forward
+ * takes w_fwd as its w_hh argument, the backward w_bwd as its w_hh_t argument. */
+int ouz_lstm_seq_pack(const float* w_hh, int32_t H, float* w_fwd, float* w_bwd, void* stream);
+int ouz_lstm_seq_fwd(const float* x_proj, const float* h0, const float* c0, const float* keep, const float* w_hh,
+                     int32_t T, int32_t B, int32_t H, float* act, float* c_all, float* hid, float* hm, float* cm,
+                     float* h_out, float* c_out, void* stream);
+int ouz_lstm_seq_bwd(const float* act, const float* c_all, const float* cm, const float* keep, const float* w_hh_t,
+                     const float* dhid, const float* dhT, const float* dcT, int32_t T, int32_t B, int32_t H,
+                     float* dgates, float* dh0, float* dc0, void* stream);
 
 /* PPO losses of one minibatch, forward + gradient for a unit upstream gradient in one call (the losses end the
  * graph).  Reductions are deterministic (fixed grid of OUZ_LOSS_BLOCKS per-block f64 partials summed in order).

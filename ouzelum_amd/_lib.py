@@ -143,6 +143,9 @@ SIGNATURES = {
     "ouz_pomdp_obs": (_I, [_P, _P, _I, _I, _I, _F, _U64, _I64, _U32, _P]),
     "ouz_lstm_cell_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
     "ouz_lstm_cell_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P]),
+    "ouz_lstm_seq_pack": (_I, [_P, _I, _P, _P, _P]),
+    "ouz_lstm_seq_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "ouz_lstm_seq_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _P]),
     "ouz_ppo_policy_loss": (_I, [_P, _P, _P, _P, _P, _I, _F, _I, _P, _P, _P, _P, _P, _P, _P]),
     "ouz_ppo_value_loss": (_I, [_P, _P, _I, _P, _P, _P, _P]),
     "ouz_tanh_bwd_bias": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),

@@ -398,6 +398,314 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// The whole done-masked LSTM recurrence of one sequence in ONE launch, forward and BPTT (RPO-LSTM/model.py:34-50;
+// torch's gate order i, f, g, o), for hidden size 128 (the reference actor's LSTM(256, 128)).  A row's carry
+// depends on that row only, so each workgroup owns 16 batch rows for all T steps and needs no grid
+// synchronisation: the carry stays on chip (c in registers, the masked h in LDS as the next step's MFMA operand)
+// instead of 2 launches + 4 B x H round trips per step.  The recurrent product runs on the f32 MFMA
+// (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulation); W_hh (256 KB) is read from L2 each step.
+//   wave w of the workgroup owns hidden units [32 w, 32 w + 32): two 16-column blocks jb, and for each the four
+//   gate tiles (columns q H + 32 w + 16 jb + [0, 16), q = i, f, g, o), so a lane's accumulators hold all four gates
+//   of its (row, unit) elements and the cell update needs no data movement.  MFMA C / D map: lane l holds rows
+//   4 (l >> 4) + r (r = 0..3) of column l & 15.  The K loop visits k in the order 16 p + 4 (l >> 4) + s
+//   (p: 16-wide slab, s = 0..3 the MFMA's step), so every lane's operands of four consecutive steps are one
+//   16-byte load (LDS for the carry / gradient tile, global for the weights).
+// ---------------------------------------------------------------------------
+constexpr int kSeqH = 128;
+constexpr int kSeqG = 4 * kSeqH;
+constexpr int kSeqRows = 16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
+}
+
+// Forward over T steps.  x_proj [T][B][4H] = x W_ih^T + b (pre-activation without the recurrent term), h0 / c0 [B][H],
+// keep [T][B] (1 - done: zeroes the carry entering step t), w [4H][H] (W_hh).  Writes, as the per-step path does,
+// act [T][B][4H] (activated gates), c_all / hid [T][B][H] and the masked carries hm / cm [T + 1][B][H] entering each
+// step (row T: the final carry, or h_out / c_out when given).  act, c_all, hm, cm may be null (inference).
+__global__ void __launch_bounds__(256) lstm_seq_fwd_kernel(
+    const float* __restrict__ xp, const float* h0, const float* c0, const float* __restrict__ keep,
+    const float* __restrict__ w, int T, int B, float* __restrict__ act, float* __restrict__ c_all,
+    float* __restrict__ hid, float* __restrict__ hm, float* __restrict__ cm, float* h_out, float* c_out) {
+  // (h_out / c_out may alias h0 / c0: each workgroup reads its rows of h0 / c0 first and writes the same rows last)
+  // the masked h entering the step (the MFMA's A operand), double-buffered by step parity so that a wave's cell
+  // update of one column block can run beside its MFMAs of the other (rows padded: conflict-free)
+  __shared__ float sh[2][kSeqRows][kSeqH + 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  const int r0 = blockIdx.x * kSeqRows;
+  for (int e = threadIdx.x; e < kSeqRows * kSeqH; e += 256) {
+    const int row = e / kSeqH, j = e - row * kSeqH, b = r0 + row;
+    const float v = b < B ? h0[(size_t)b * kSeqH + j] * keep[b] : 0.0f;
+    sh[0][row][j] = v;
+    if (hm && b < B) hm[(size_t)b * kSeqH + j] = v;
+  }
+  float c[2][4];
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = r0 + 4 * lg + r, j = 32 * wv + 16 * jb + li;
+      c[jb][r] = b < B ? c0[(size_t)b * kSeqH + j] * keep[b] : 0.0f;
+      if (cm && b < B) cm[(size_t)b * kSeqH + j] = c[jb][r];
+    }
+  // the wave's weight fragments, packed by ouz_lstm_seq_pack in the order the lanes consume them (wf [wave][slab]
+  // [jb][q][lane] f32x4): every fragment load is one contiguous 1 KB (eight full cache lines) per wave.
+  // The wave's whole weight slice (128 gate columns x 128, 64 KB: 256 registers per lane) is loaded once and kept in
+  // registers for all T steps (one wave per SIMD: the register file has room), so the steps read no weights at all.
+  const f32x4* wl = reinterpret_cast<const f32x4*>(w) + (size_t)wv * (kSeqH / 16) * 8 * 64 + lane;
+  f32x4 wreg[kSeqH / 16][2][4];
+#pragma unroll
+  for (int p = 0; p < kSeqH / 16; ++p)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wreg[p][jb][q] = wl[((size_t)p * 8 + jb * 4 + q) * 64];
+  // this lane's rows and their validity (a ragged last workgroup computes zero rows and stores nothing for them)
+  int rb[4];
+  bool rv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    rb[r] = r0 + 4 * lg + r;
+    rv[r] = rb[r] < B;
+  }
+  // A step's inputs (its input projection, the next step's keep) are loaded one step ahead, before the previous
+  // step's output stores: gfx950's single vmcnt counter retires loads and stores in order, so loads issued after
+  // a step's 64 stores could not be waited for without waiting for those stores too (SQ_WAIT_INST_ANY was 41 %
+  // of the wave's cycles with the loads at the top of the step).
+  float x[2][4][4], kn[4], xn[2][4][4], knn[4];
+  const auto load_inputs = [&](int t, float (&xd)[2][4][4], float (&kd)[4]) {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          xd[jb][q][r] = rv[r] ? xp[((size_t)t * B + rb[r]) * kSeqG + q * kSeqH + 32 * wv + 16 * jb + li] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kd[r] = (t + 1 < T && rv[r]) ? keep[(size_t)(t + 1) * B + rb[r]] : 1.0f;
+  };
+  load_inputs(0, x, kn);
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1;
+    const bool last = t == T - 1;
+    __syncthreads();   // sh[cur] holds this step's carry (and every wave is done with sh[cur ^ 1])
+    float ig[2][4], fg[2][4], gg[2][4], og[2][4], cn[2][4], hn[2][4];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      // the product of column block jb; block 0's cell update below is independent of block 1's MFMAs, so the
+      // scheduler can issue its VALU work while those run
+      f32x4 acc[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int p = 0; p < kSeqH / 16; ++p) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&sh[cur][li][16 * p + 4 * lg]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] = mfma4(a, wreg[p][jb][q], acc[q]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        // gates = x_proj + h W_hh^T (the GEMM path's beta = 1 accumulation: the projection added to the product)
+        ig[jb][r] = sigm(x[jb][0][r] + acc[0][r]);
+        fg[jb][r] = sigm(x[jb][1][r] + acc[1][r]);
+        gg[jb][r] = tanhf(x[jb][2][r] + acc[2][r]);
+        og[jb][r] = sigm(x[jb][3][r] + acc[3][r]);
+        cn[jb][r] = fg[jb][r] * c[jb][r] + ig[jb][r] * gg[jb][r];
+        hn[jb][r] = og[jb][r] * tanhf(cn[jb][r]);
+        const float hmv = kn[r] * hn[jb][r];
+        c[jb][r] = kn[r] * cn[jb][r];
+        sh[cur ^ 1][4 * lg + r][32 * wv + 16 * jb + li] = hmv;
+      }
+    }
+    if (!last) load_inputs(t + 1, xn, knn);   // ahead of this step's stores
+    float knc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) knc[r] = kn[r];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!rv[r]) continue;
+        const int b = rb[r], j = 32 * wv + 16 * jb + li;
+        const size_t base = (size_t)t * B + b;
+        if (act) {
+          float* a = act + base * kSeqG;
+          a[j] = ig[jb][r]; a[kSeqH + j] = fg[jb][r]; a[2 * kSeqH + j] = gg[jb][r]; a[3 * kSeqH + j] = og[jb][r];
+        }
+        if (c_all) c_all[base * kSeqH + j] = cn[jb][r];
+        hid[base * kSeqH + j] = hn[jb][r];
+        const float hmv = knc[r] * hn[jb][r];
+        if (last && h_out) {
+          h_out[(size_t)b * kSeqH + j] = hmv;
+          c_out[(size_t)b * kSeqH + j] = c[jb][r];
+        } else {
+          const size_t nx = ((size_t)(t + 1) * B + b) * kSeqH + j;
+          if (hm) hm[nx] = hmv;
+          if (cm) cm[nx] = c[jb][r];
+        }
+      }
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[jb][q][r] = xn[jb][q][r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kn[r] = knn[r];
+  }
+}
+
+// BPTT over T steps (the mirror of lstm_seq_fwd_kernel and of the per-step lstm_cell_bwd_kernel + GEMM): per step
+// dh = dhid + keep_{t+1} G with G = dgates_{t+1} W_hh (the MFMA product, K = 4H, from the dgates tile kept in LDS;
+// at t = T - 1 G is dhT, or nothing), dc = keep_{t+1} dc_next + dh o (1 - tanh(c)^2).  Writes dgates [T][B][4H]
+// (pre-activation), dh0 = (dgates_0 W_hh) keep_0 and dc0 = dc keep_0 [B][H].  wt = W_hh^T [H][4H] (contiguous), so
+// the weight fragments are 16-byte loads along k.
+__global__ void __launch_bounds__(256) lstm_seq_bwd_kernel(
+    const float* __restrict__ act, const float* __restrict__ c_all, const float* __restrict__ cm,
+    const float* __restrict__ keep, const float* __restrict__ wt, const float* __restrict__ dhid,
+    const float* __restrict__ dhT, const float* __restrict__ dcT, int T, int B, float* __restrict__ dgates,
+    float* __restrict__ dh0, float* __restrict__ dc0) {
+  // dgates of the step after (A operand of G), double-buffered by step parity: a wave's cell update of one column
+  // block runs beside its MFMAs of the other, one barrier per step
+  __shared__ float sg[2][kSeqRows][kSeqG + 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
+  const int r0 = blockIdx.x * kSeqRows;
+  // packed W_hh^T fragments (ouz_lstm_seq_pack: wb [wave][slab][jb][lane] f32x4, one contiguous 1 KB per load): the
+  // wave's slice (32 hidden units x 512 gate columns, 64 KB: 256 registers per lane) is loaded once for all T steps
+  const f32x4* wl = reinterpret_cast<const f32x4*>(wt) + (size_t)wv * (kSeqG / 16) * 2 * 64 + lane;
+  f32x4 wreg[kSeqG / 16][2];
+#pragma unroll
+  for (int p = 0; p < kSeqG / 16; ++p) {
+    wreg[p][0] = wl[(size_t)p * 128];
+    wreg[p][1] = wl[(size_t)p * 128 + 64];
+  }
+  // G of column block jb = sg[buf] W_hh over the 4H gate columns
+  const auto product = [&](int buf, int jb) {
+    f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int p = 0; p < kSeqG / 16; ++p) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(&sg[buf][li][16 * p + 4 * lg]);
+      acc = mfma4(a, wreg[p][jb], acc);
+    }
+    return acc;
+  };
+  int rb[4];
+  bool rv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    rb[r] = r0 + 4 * lg + r;
+    rv[r] = rb[r] < B;
+  }
+  float dc[2][4];
+  // the cell's saved values of a step are loaded one step ahead, before the later step's dgates stores (one
+  // in-order vmcnt counter for loads and stores: see lstm_seq_fwd_kernel)
+  float ag[2][4][4], cv[2][4], cp[2][4], dy[2][4], kn[4];
+  const auto load_saved = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) kn[r] = (t + 1 < T && rv[r]) ? keep[(size_t)(t + 1) * B + rb[r]] : 1.0f;
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 32 * wv + 16 * jb + li;
+        const size_t base = (size_t)t * B + rb[r];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ag[jb][q][r] = rv[r] ? act[base * kSeqG + q * kSeqH + j] : 0.0f;
+        cv[jb][r] = rv[r] ? c_all[base * kSeqH + j] : 0.0f;
+        cp[jb][r] = rv[r] ? cm[base * kSeqH + j] : 0.0f;
+        dy[jb][r] = rv[r] ? dhid[base * kSeqH + j] : 0.0f;
+      }
+  };
+  load_saved(T - 1);
+  for (int t = T - 1; t >= 0; --t) {
+    const bool lastt = t == T - 1;
+    const int cur = t & 1;   // the buffer this step writes; it reads cur ^ 1 (written by step t + 1)
+    const bool has_g = !lastt || dhT != nullptr;
+    const bool has_dc = !lastt || dcT != nullptr;
+    // sg[cur ^ 1] holds dgates_{t+1}, and every wave is done with sg[cur] (read by step t + 1)
+    if (!lastt) __syncthreads();
+    float di[2][4], df[2][4], dg[2][4], d_o[2][4];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      f32x4 acc;
+      if (lastt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[r] = (dhT && rv[r]) ? dhT[(size_t)rb[r] * kSeqH + 32 * wv + 16 * jb + li] : 0.0f;
+      } else {
+        acc = product(cur ^ 1, jb);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 32 * wv + 16 * jb + li;
+        const float k = kn[r];
+        const float dcn = lastt ? ((dcT && rv[r]) ? dcT[(size_t)rb[r] * kSeqH + j] : 0.0f) : dc[jb][r];
+        const float dh = dy[jb][r] + (has_g ? k * acc[r] : 0.0f);
+        const float ig = ag[jb][0][r], fg = ag[jb][1][r], gg = ag[jb][2][r], og = ag[jb][3][r];
+        const float tc = tanhf(cv[jb][r]);
+        const float dcv = (has_dc ? k * dcn : 0.0f) + dh * og * (1.0f - tc * tc);
+        di[jb][r] = dcv * gg * ig * (1.0f - ig);
+        df[jb][r] = dcv * cp[jb][r] * fg * (1.0f - fg);
+        dg[jb][r] = dcv * ig * (1.0f - gg * gg);
+        d_o[jb][r] = dh * tc * og * (1.0f - og);
+        float* srow = sg[cur][4 * lg + r];
+        srow[j] = di[jb][r]; srow[kSeqH + j] = df[jb][r]; srow[2 * kSeqH + j] = dg[jb][r];
+        srow[3 * kSeqH + j] = d_o[jb][r];
+        dc[jb][r] = dcv * fg;
+      }
+    }
+    if (t > 0) load_saved(t - 1);   // ahead of this step's stores (the values above are consumed)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (!rv[r]) continue;
+        const int j = 32 * wv + 16 * jb + li;
+        float* d = dgates + ((size_t)t * B + rb[r]) * kSeqG;
+        d[j] = di[jb][r]; d[kSeqH + j] = df[jb][r]; d[2 * kSeqH + j] = dg[jb][r]; d[3 * kSeqH + j] = d_o[jb][r];
+      }
+  }
+  // dh0 = (dgates_0 W_hh) keep_0, dc0 = dc keep_0
+  __syncthreads();
+#pragma unroll
+  for (int jb = 0; jb < 2; ++jb) {
+    const f32x4 acc = product(0, jb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!rv[r]) continue;
+      const int j = 32 * wv + 16 * jb + li;
+      const float k0 = keep[rb[r]];
+      if (dh0) dh0[(size_t)rb[r] * kSeqH + j] = acc[r] * k0;
+      if (dc0) dc0[(size_t)rb[r] * kSeqH + j] = dc[jb][r] * k0;
+    }
+  }
+}
+
+// The weight fragments of lstm_seq_fwd_kernel / lstm_seq_bwd_kernel in consumption order (one thread per f32x4):
+//   wf[w][p][jb][q][l] = W_hh[q H + 32 w + 16 jb + (l & 15)][16 p + 4 (l >> 4) + 0..3]        (8 slabs of K = H)
+//   wb[w][p][jb][l]    = W_hh[16 p + 4 (l >> 4) + 0..3][32 w + 16 jb + (l & 15)]              (32 slabs of K = 4H)
+__global__ void __launch_bounds__(256) lstm_seq_pack_kernel(const float* __restrict__ w, f32x4* __restrict__ wf,
+                                                            f32x4* __restrict__ wb) {
+  const int e = blockIdx.x * 256 + threadIdx.x;   // kSeqH * kSeqG / 4 fragments per layout
+  if (e >= kSeqH * kSeqG / 4) return;
+  {
+    const int l = e & 63, q = (e >> 6) & 3, jb = (e >> 8) & 1, p = (e >> 9) & 7, wv = e >> 12;
+    const float* src = w + (size_t)(q * kSeqH + 32 * wv + 16 * jb + (l & 15)) * kSeqH + 16 * p + 4 * (l >> 4);
+    wf[e] = f32x4{src[0], src[1], src[2], src[3]};
+  }
+  {
+    const int l = e & 63, jb = (e >> 6) & 1, p = (e >> 7) & 31, wv = e >> 12;
+    const int n = 32 * wv + 16 * jb + (l & 15), k = 16 * p + 4 * (l >> 4);
+    wb[e] = f32x4{w[(size_t)k * kSeqH + n], w[(size_t)(k + 1) * kSeqH + n], w[(size_t)(k + 2) * kSeqH + n],
+                  w[(size_t)(k + 3) * kSeqH + n]};
+  }
+}
+
 inline int grid(int n, int b) { return (n + b - 1) / b; }
 
 int launch_status(const char* what) {
@@ -456,6 +764,45 @@ int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* ke
   hipLaunchKernelGGL(lstm_cell_fwd_kernel, dim3(grid(B * H, 256)), dim3(256), 0, (hipStream_t)stream, gates, c_prev_m,
                      keep_next, act, c_out, h_out, h_next_m, c_next_m, B, H);
   return launch_status("lstm_cell_fwd_kernel");
+}
+
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int ouz_lstm_seq_pack(const float* w_hh, int32_t H, float* w_fwd, float* w_bwd, void* stream) {
+  if (H != kSeqH) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_pack: H must be 128");
+  if (!w_hh || !w_fwd || !w_bwd) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_pack: null buffer");
+  if (!aligned16(w_fwd) || !aligned16(w_bwd))
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_pack: packed buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(lstm_seq_pack_kernel, dim3(grid(kSeqH * kSeqG / 4, 256)), dim3(256), 0, (hipStream_t)stream, w_hh,
+                     reinterpret_cast<f32x4*>(w_fwd), reinterpret_cast<f32x4*>(w_bwd));
+  return launch_status("lstm_seq_pack_kernel");
+}
+
+int ouz_lstm_seq_fwd(const float* x_proj, const float* h0, const float* c0, const float* keep, const float* w_hh,
+                     int32_t T, int32_t B, int32_t H, float* act, float* c_all, float* hid, float* hm, float* cm,
+                     float* h_out, float* c_out, void* stream) {
+  if (H != kSeqH) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: H must be 128");
+  if (T <= 0 || B <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: T and B must be > 0");
+  if (!x_proj || !h0 || !c0 || !keep || !w_hh || !hid || (!h_out) != (!c_out))
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: null buffer (h_out and c_out: both or neither)");
+  if (!aligned16(w_hh)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: w_fwd must be 16-byte aligned");
+  hipLaunchKernelGGL(lstm_seq_fwd_kernel, dim3(grid(B, kSeqRows)), dim3(256), 0, (hipStream_t)stream, x_proj, h0, c0,
+                     keep, w_hh, T, B, act, c_all, hid, hm, cm, h_out, c_out);
+  return launch_status("lstm_seq_fwd_kernel");
+}
+
+int ouz_lstm_seq_bwd(const float* act, const float* c_all, const float* cm, const float* keep, const float* w_hh_t,
+                     const float* dhid, const float* dhT, const float* dcT, int32_t T, int32_t B, int32_t H,
+                     float* dgates, float* dh0, float* dc0, void* stream) {
+  if (H != kSeqH) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: H must be 128");
+  if (T <= 0 || B <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: T and B must be > 0");
+  if (!act || !c_all || !cm || !keep || !w_hh_t || !dhid || !dgates)
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: null buffer");
+  if (!aligned16(w_hh_t)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: w_bwd must be 16-byte aligned");
+  hipLaunchKernelGGL(lstm_seq_bwd_kernel, dim3(grid(B, kSeqRows)), dim3(256), 0, (hipStream_t)stream, act, c_all, cm,
+                     keep, w_hh_t, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
+  return launch_status("lstm_seq_bwd_kernel");
 }
 
 int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, const float* dhid, const float* G,

@@ -1,11 +1,12 @@
 """GPU-side building blocks of the recurrent learner (HIP + hipBLASLt), with autograd.
 
 * ``LSTMSequence``: the whole done-masked recurrence of ``RPO-LSTM/model.py:34-50`` over T
-  steps.  Per step one hipBLASLt GEMM (h W_hh^T added onto the precomputed input projection)
-  and ONE fused HIP cell kernel (``ouz_lstm_cell_fwd``); BPTT is the mirror image
-  (``ouz_lstm_cell_bwd`` + one GEMM per step) and dW_hh is one split-K product over all
-  T·B rows.  torch's per-step nn.LSTM costs ~10 element-wise launches forward and ~20
-  backward per step.
+  steps.  For the reference's hidden size 128: ONE launch forward (``ouz_lstm_seq_fwd``) and one for BPTT
+  (``ouz_lstm_seq_bwd``), each workgroup carrying 16 batch rows through all T steps with the recurrent product
+  on the f32 MFMA (round 6).  Otherwise per step one hipBLASLt GEMM (h W_hh^T added onto the precomputed input
+  projection) and ONE fused HIP cell kernel (``ouz_lstm_cell_fwd``); BPTT is the mirror image
+  (``ouz_lstm_cell_bwd`` + one GEMM per step).  dW_hh is one split-K product over all T·B rows either way.
+  torch's per-step nn.LSTM costs ~10 element-wise launches forward and ~20 backward per step.
 * ``splitk_wgrad`` / ``SplitKLinear``: weight gradients dW = dYᵀ X with K = T·B rows
   (32 768 at the reference's 16 x 4096 minibatch halves) and a small output (512 x 256):
   a plain GEMM puts 16 output tiles on 256 CUs; splitting K into S slabs and summing
@@ -23,6 +24,10 @@ import torch
 from .. import _lib as L
 
 _INPLACE_GATES = os.environ.get("OUZ_LSTM_INPLACE_GATES", "1") != "0"
+# the whole recurrence in one launch each way (ouz_lstm_seq_fwd / _bwd) where H = 128; OUZ_LSTM_SEQ=0 keeps the
+# per-step GEMM + cell kernel pairs
+_SEQ = os.environ.get("OUZ_LSTM_SEQ", "1") != "0"
+SEQ_H = 128
 _FUSED_TANH = os.environ.get("OUZ_FUSED_TANH", "1") != "0"
 _FUSED_SAMPLE = os.environ.get("OUZ_FUSED_SAMPLE", "1") != "0"
 
@@ -212,11 +217,58 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
-def _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=None):
-    """The T-step recurrence: per step the recurrent GEMM onto the input projection and one fused cell launch.
-    Returns (act, c_all, hid, hm, cm, keep).  ``carry_out=(h, c)``: the last step writes the final carry (keep = 1,
-    so the masked next-step carry is the carry itself) into these buffers instead of the scratch row; they may
-    alias h0 / c0, which are consumed (masked into hm[0] / cm[0]) before any cell launch."""
+SEQ_MIN_T = 4
+
+
+def seq_kernels_ok(x_proj):
+    """The fused sequence kernels apply: hidden size 128 (the reference actor's), f32, and a sequence of at least
+    SEQ_MIN_T steps.  Each workgroup loads its 256 KB of weight fragments once per launch and keeps them in registers,
+    which pays over a sequence (the update's T = 16); the rollout's one-step policy calls keep the GEMM + cell pair."""
+    return (_SEQ and x_proj.shape[-1] == 4 * SEQ_H and x_proj.dtype == torch.float32
+            and x_proj.shape[0] >= SEQ_MIN_T)
+
+
+def seq_pack(w_hh):
+    """W_hh in the sequence kernels' two fragment layouts (ouz_lstm_seq_pack): (w_fwd, w_bwd)."""
+    w = w_hh.detach().contiguous()
+    wf, wb = torch.empty_like(w), torch.empty_like(w)
+    L.check(L.lib.ouz_lstm_seq_pack(w.data_ptr(), w.shape[1], wf.data_ptr(), wb.data_ptr(), L.stream_ptr(w.device)),
+            "ouz_lstm_seq_pack")
+    return wf, wb
+
+
+def _lstm_forward_seq(x_proj, h0, c0, keep, w_hh, carry_out=None, saved=True, packed=None):
+    """``_lstm_forward`` as ONE launch (ouz_lstm_seq_fwd): the carry stays on chip across the T steps.  ``saved=False``
+    (inference) skips the tensors only BPTT reads.  ``packed``: seq_pack(w_hh), made here when not given."""
+    T, B, G4 = x_proj.shape
+    H = G4 // 4
+    dev = x_proj.device
+    x_proj = x_proj.contiguous()
+    keep = keep.contiguous().float()
+    h0, c0 = h0.contiguous(), c0.contiguous()
+    w = (packed or seq_pack(w_hh))[0]
+    hid = torch.empty((T, B, H), device=dev)
+    act = c_all = hm = cm = None
+    if saved:
+        act = torch.empty((T, B, G4), device=dev)
+        c_all = torch.empty((T, B, H), device=dev)
+        hm = torch.empty((T + 1, B, H), device=dev)
+        cm = torch.empty((T + 1, B, H), device=dev)
+    ho, co = carry_out if carry_out is not None else (None, None)
+    L.check(L.lib.ouz_lstm_seq_fwd(x_proj.data_ptr(), h0.data_ptr(), c0.data_ptr(), keep.data_ptr(), w.data_ptr(),
+                                   T, B, H, _p(act), _p(c_all), hid.data_ptr(), _p(hm), _p(cm), _p(ho), _p(co),
+                                   L.stream_ptr(dev)), "ouz_lstm_seq_fwd")
+    return act, c_all, hid, hm, cm, keep
+
+
+def _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=None, saved=True):
+    """The T-step recurrence: per step the recurrent GEMM onto the input projection and one fused cell launch
+    (or all T steps in one launch, ``_lstm_forward_seq``, where ``seq_kernels_ok``).  Returns (act, c_all, hid, hm,
+    cm, keep).  ``carry_out=(h, c)``: the last step writes the final carry (keep = 1, so the masked next-step carry is
+    the carry itself) into these buffers instead of the scratch row; they may alias h0 / c0, which are consumed
+    (masked into hm[0] / cm[0]) before any cell launch."""
+    if seq_kernels_ok(x_proj):
+        return _lstm_forward_seq(x_proj, h0, c0, keep, w_hh, carry_out, saved)
     T, B, G4 = x_proj.shape
     H = G4 // 4
     dev = x_proj.device
@@ -260,7 +312,7 @@ def lstm_sequence_carry_inplace(x_proj, h0, c0, keep, w_hh, h_out, c_out):
     for t, name in ((h_out, "h_out"), (c_out, "c_out")):
         if not t.is_contiguous() or tuple(t.shape[-2:]) != (x_proj.shape[1], x_proj.shape[2] // 4):
             raise ValueError(f"lstm_sequence_carry_inplace: {name} must be a contiguous (B, H) buffer")
-    return _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=(h_out, c_out))[2]
+    return _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=(h_out, c_out), saved=False)[2]
 
 
 class LSTMSequence(torch.autograd.Function):
@@ -270,7 +322,10 @@ class LSTMSequence(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_proj, h0, c0, keep, w_hh):
         ctx.set_materialize_grads(False)     # unused h_T / c_T come back as None, not zero-filled tensors
-        act, c_all, hid, hm, cm, keep = _lstm_forward(x_proj, h0, c0, keep, w_hh)
+        packed = seq_pack(w_hh) if seq_kernels_ok(x_proj) else None
+        act, c_all, hid, hm, cm, keep = (_lstm_forward_seq(x_proj, h0, c0, keep, w_hh, packed=packed) if packed
+                                         else _lstm_forward(x_proj, h0, c0, keep, w_hh))
+        ctx.packed_bwd = packed[1] if packed else None
         ctx.save_for_backward(act, c_all, cm, hm, keep, w_hh)
         T = hid.shape[0]
         return hid, hid[T - 1].clone(), c_all[T - 1].clone()
@@ -288,6 +343,18 @@ class LSTMSequence(torch.autograd.Function):
         dhT = dhT.contiguous() if dhT is not None else None
         dcT = dcT.contiguous() if dcT is not None else None
         dgates = torch.empty((T, B, G4), device=dev)
+        if ctx.packed_bwd is not None:
+            # BPTT of all T steps in one launch (ouz_lstm_seq_bwd); dW_hh stays one split-K product over T·B rows
+            wt = ctx.packed_bwd
+            ctx.packed_bwd = None
+            dh0 = torch.empty((B, H), device=dev) if ctx.needs_input_grad[1] else None
+            dc0 = torch.empty((B, H), device=dev) if ctx.needs_input_grad[2] else None
+            L.check(L.lib.ouz_lstm_seq_bwd(act.data_ptr(), c_all.data_ptr(), cm.data_ptr(), keep.data_ptr(),
+                                           wt.data_ptr(), dhid.data_ptr(), _p(dhT), _p(dcT), T, B, H,
+                                           dgates.data_ptr(), _p(dh0), _p(dc0), stream), "ouz_lstm_seq_bwd")
+            d_w = (splitk_wgrad(dgates.view(T * B, G4), hm[:T].reshape(T * B, H)) if ctx.needs_input_grad[4]
+                   else None)
+            return dgates, dh0, dc0, None, d_w
         G = torch.empty((B, H), device=dev)
         dc = torch.empty((B, H), device=dev)
         for t in range(T - 1, -1, -1):

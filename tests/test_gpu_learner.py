@@ -170,6 +170,55 @@ def test_fused_lstm_and_splitk_gradients_match_torch():
     assert max(errs.values()) < 2e-4, errs
 
 
+@pytest.mark.parametrize("T,B", [(16, 1000), (4, 8192), (5, 8), (16, 4096)])
+def test_lstm_seq_kernels_match_per_step_path(T, B, monkeypatch):
+    """The one-launch recurrence (ouz_lstm_seq_fwd / _bwd: 16 rows per workgroup through all T steps, the recurrent
+    product on the f32 MFMA) against the per-step hipBLASLt GEMM + cell-kernel path (OUZ_LSTM_SEQ=0) and against
+    float64 torch autograd of the reference cell (model.py:34-50): hidden outputs, final carry, and the gradients of
+    x_proj, h0, c0 and W_hh, with done masks; ragged B (not a multiple of 16, fewer than 16 rows), the shortest
+    sequence the kernels take (fused.SEQ_MIN_T) over two workgroups per CU, and the reference's 16 x 4096 minibatch.  f32 tolerance: the products sum in another
+    order than hipBLASLt's."""
+    from ouzelum_amd.learners import fused as F
+    assert T >= F.SEQ_MIN_T
+    g = torch.Generator(device="cuda").manual_seed(T * 7 + B)
+    H = 128
+    xp = torch.randn((T, B, 4 * H), device="cuda", generator=g)
+    h0 = torch.randn((B, H), device="cuda", generator=g) * 0.5
+    c0 = torch.randn((B, H), device="cuda", generator=g) * 0.5
+    keep = (torch.rand((T, B), device="cuda", generator=g) > 0.1).float()
+    w = torch.randn((4 * H, H), device="cuda", generator=g) * (1.0 / H ** 0.5)
+    up = [torch.randn((T, B, H), device="cuda", generator=g), torch.randn((B, H), device="cuda", generator=g),
+          torch.randn((B, H), device="cuda", generator=g)]
+
+    def run(seq, dtype=torch.float32):
+        ins = [t.detach().to(dtype).clone().requires_grad_(True) for t in (xp, h0, c0, w)]
+        if dtype == torch.float64:   # the reference cell in f64
+            h, c = ins[1] * keep[0].double().unsqueeze(1), ins[2] * keep[0].double().unsqueeze(1)
+            outs = []
+            for t in range(T):
+                if t > 0:
+                    h, c = h * keep[t].double().unsqueeze(1), c * keep[t].double().unsqueeze(1)
+                i, f, gg, o = (ins[0][t] + h @ ins[3].t()).chunk(4, dim=1)
+                c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+                h = torch.sigmoid(o) * torch.tanh(c)
+                outs.append(h)
+            hid, hT, cT = torch.stack(outs), h, c
+        else:
+            monkeypatch.setattr(F, "_SEQ", seq)
+            hid, hT, cT = F.LSTMSequence.apply(ins[0], ins[1], ins[2], keep, ins[3])
+        loss = (hid * up[0].to(dtype)).sum() + (hT * up[1].to(dtype)).sum() + (cT * up[2].to(dtype)).sum()
+        loss.backward()
+        return [hid.detach().double(), hT.detach().double(), cT.detach().double()] + [t.grad.double() for t in ins]
+
+    names = ["hid", "h_T", "c_T", "d x_proj", "d h0", "d c0", "d W_hh"]
+    seq, per, ref = run(True), run(False), run(None, torch.float64)
+    for n, a, b, r in zip(names, seq, per, ref):
+        scale = r.abs().max().clamp_min(1e-6)
+        e_seq, e_per = float((a - r).abs().max() / scale), float((b - r).abs().max() / scale)
+        # the fused path is as close to f64 as the per-step f32 path is (a few ulp of the largest entry)
+        assert e_seq < 1e-4 and e_seq < 4 * e_per + 1e-5, (n, e_seq, e_per)
+
+
 @pytest.mark.parametrize("recurrent,alias", [(True, False), (False, False), (True, True)])
 def test_graphed_policy_matches_eager(recurrent, alias, monkeypatch):
     """PPOLearner.act (the rollout step's policy replayed from a hipGraph) against the eager policy
