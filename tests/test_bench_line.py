@@ -114,7 +114,7 @@ def _csv_avg_us(path, kernel):
     import csv
     with open(path) as fh:
         for row in csv.DictReader(fh):
-            if row["Name"].startswith(kernel + "<"):
+            if ("::" + kernel + "<") in row["Name"] or row["Name"].startswith(kernel + "<"):
                 return float(row["AverageNs"]) / 1e3
     return None
 
@@ -138,7 +138,9 @@ def test_rocprof_priced_fraction_recomputes_from_committed_files():
         if d.get("mixed_split") or not d.get("rocprof_avg_us"):
             continue
         task, n = d["task"], d["num_envs"]
-        kernel = "rollout" if d["kernel"] == "quad_rollout_kernel" else "step"
+        kernel = "rollout" if "_rollout_" in os.path.basename(h) else "step"
+        if kernel == "rollout" and B.streamed_rollout(task, n):
+            continue   # step launches + copies + statistics: bench.py prices no rocprof fraction for it
         csv_path = h[:-len("_summary.json")] + "_kernel_stats.csv"
         us = _csv_avg_us(csv_path, d["kernel"])
         if kernel == "step" and us is None:
@@ -148,8 +150,6 @@ def test_rocprof_priced_fraction_recomputes_from_committed_files():
         alg = (B.rollout_bytes_per_env_step(task, steps) if kernel == "rollout"
                else B.BYTES_PER_ENV_STEP[task] + B.EPISODE_TRACK_BYTES) * n * steps
         want = alg / (us * 1e-6) / 1e9 / B.HBM_PEAK_GBPS
-        if kernel == "rollout" and B.streamed_rollout(task, n):
-            continue
         got = B.price_summary(d, kernel, task, n)
         assert abs(got["frac_from_rocprof_avg"] - want) <= 0.01 * want, (h, got, want)
         assert abs(got["traffic_alg_ratio"] - d["traffic_bytes_per_launch"] / alg) <= 1e-3, h
