@@ -43,7 +43,9 @@ def roofline_table(d):
         pmc = td.get("bytes_per_env_step")
         rw = (f"{pmc:.1f} ({td['read_bytes_per_env_step']:.1f} + {td['write_bytes_per_env_step']:.1f})"
               if pmc is not None else ("stale" if td.get("stale") else "-"))
-        ratio = pmc / e["bytes_per_env_step"] if pmc else None
+        # PMC traffic against the algorithmic bytes of the SAME launch (the summary's own launch length: bench.py
+        # price_summary), not of the priced region's launches
+        ratio = e.get("traffic_alg_ratio") or (pmc / e["bytes_per_env_step"] if pmc else None)
         kern = e["kernel"].replace("quad_", "").replace("_kernel", "")
         if e.get("steps_per_rollout"):
             kern = "rollout (streamed step launches)"

@@ -538,8 +538,9 @@ def test_vectask_dr_noise_parity(ouz, obs_p, act_p, freq):
         ok = ~near_threshold(o)
         assert_close(f"drn@{k} obs", g["obs"][ok], r["obs"][ok], 1e-4, 1e-5)
         assert_close(f"drn@{k} thrust", g["thrust"], r["thrust"], 1e-3, 1e-6)
-    with pytest.raises(NotImplementedError):
-        env.apply_randomizations({"sim_params": {}})
+    with pytest.raises(NotImplementedError):   # PhysX solver parameters (sim_params.gravity is built: test_dr_physical)
+        env.apply_randomizations({"sim_params": {"rest_offset": {"range": [0.0, 0.01], "operation": "additive",
+                                                                 "distribution": "uniform"}}})
 
 
 @pytest.mark.parametrize("task", ["QuadTracking", "QuadMixed"])
