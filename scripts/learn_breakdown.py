@@ -26,6 +26,8 @@ def category(name):
         return "runtime copy / fill"
     if "lstm_cell" in name:
         return "lstm cell (HIP)"
+    if "lstm_seq" in name:
+        return "lstm recurrence, one launch per direction (HIP, f32 MFMA)"
     if any(k in name for k in ("policy_loss_kernel", "value_loss_kernel", "loss_finish_kernel", "adv_moments_kernel",
                                 "tanh_bwd_colsum_kernel", "colsum_finish_kernel")):
         return "PPO losses + trunk tanh'/bias (HIP)"
