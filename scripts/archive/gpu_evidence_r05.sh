@@ -1,13 +1,13 @@
 #!/bin/bash
 # Round-5 evidence of ONE library build, in gpurun calls each under the 20-minute limit:
-#   bash scripts/gpu_evidence_r05.sh TAG h   the headline alone (when boxes are scarce): roofline + VALU evidence of
+#   bash scripts/archive/gpu_evidence_r05.sh TAG h   the headline alone (when boxes are scarce): roofline + VALU evidence of
 #                                            config B's two kernels, staged, then smoke(), the driver-argument bench
 #                                            line and rocprofv3 --stats of the driver's command
-#   bash scripts/gpu_evidence_r05.sh TAG t   GPU suite and smoke()
-#   bash scripts/gpu_evidence_r05.sh TAG a   (after h) roofline evidence (rocprofv3 --stats + FETCH_SIZE /
+#   bash scripts/archive/gpu_evidence_r05.sh TAG t   GPU suite and smoke()
+#   bash scripts/archive/gpu_evidence_r05.sh TAG a   (after h) roofline evidence (rocprofv3 --stats + FETCH_SIZE /
 #                                            WRITE_SIZE passes) of the headline-size entries, VALU / issue passes
 #                                            of every entry that is not HBM-bound
-#   bash scripts/gpu_evidence_r05.sh TAG b   roofline evidence of the large-N sweep, then the bench lines (driver
+#   bash scripts/archive/gpu_evidence_r05.sh TAG b   roofline evidence of the large-N sweep, then the bench lines (driver
 #                                            arguments, no flags) and rocprofv3 --stats of the driver's command
 # Summaries land in gpurun_out/ (copied into profiles/r05/ by hand between the calls; part b stages its own into
 # profiles/r05/roofline on the box so that its bench lines price traffic from them).  Stops at the first failure.

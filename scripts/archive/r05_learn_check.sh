@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5: learner GPU tests and the config D bench on the current library, then (same library) the headline
-# evidence part of scripts/gpu_evidence_r05.sh.   bash scripts/archive/r05_learn_check.sh TAG
+# evidence part of scripts/archive/gpu_evidence_r05.sh.   bash scripts/archive/r05_learn_check.sh TAG
 set -u
 TAG=$1
 O=gpurun_out/$TAG
@@ -16,4 +16,4 @@ for r in 1 2 3; do
   echo "round $r: $(cat $O/learn_$r.json)"
 done
 bash scripts/archive/r05_learn_prof.sh $TAG > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
-bash scripts/gpu_evidence_r05.sh $TAG h
+bash scripts/archive/gpu_evidence_r05.sh $TAG h
