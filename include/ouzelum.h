@@ -67,7 +67,8 @@ extern "C" {
                                5: learner kernels (ouz_ppo_policy_loss, ouz_ppo_value_loss, ouz_tanh_bwd_bias,
                                   ouz_policy_sample);
                                6: sim_params gravity domain randomisation (ouz_set_dr_gravity), the fused LSTM
-                                  sequence kernels (ouz_lstm_seq_fwd / ouz_lstm_seq_bwd) */
+                                  sequence kernels (ouz_lstm_seq_fwd / ouz_lstm_seq_bwd), clipped Adam
+                                  (ouz_adam_clip_step) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -424,7 +425,9 @@ int ouz_lstm_cell_bwd(const float* act, const float* c, const float* c_prev_m, c
  * carry unless h_out / c_out [B][H] take it, which may alias h0 / c0).  Backward: the saved act / c_all / cm, keep,
  * the packed W_hh^T (w_bwd of ouz_lstm_seq_pack), dhid [T][B][H], dhT / dcT [B][H] or null; writes dgates
  * [T][B][4H] and, when not null, dh0 = (dgates_0 W_hh) keep_0 and dc0 [B][H].  Same arithmetic per element as the
- * per-step kernels; the products sum in another order (f32, within rounding of the GEMM path). */
+ * per-step kernels; the products sum in another order (f32, within rounding of the GEMM path).  Every buffer except
+ * keep and h0 (x_proj, c0, the outputs, the saved tensors and gradients) must be 16-byte aligned (one 16-byte access
+ * per lane); OUZ_ERR_INVALID otherwise. */
 /* ouz_lstm_seq_pack: W_hh [4H][H] into the two fragment layouts the sequence kernels read (w_fwd, w_bwd: 4H * H
  * floats each, 16-byte aligned; one contiguous 1 KB per wave per load), after every change of W_hh.  The forward
  * takes w_fwd as its w_hh argument, the backward w_bwd as its w_hh_t argument. */
@@ -435,6 +438,24 @@ int ouz_lstm_seq_fwd(const float* x_proj, const float* h0, const float* c0, cons
 int ouz_lstm_seq_bwd(const float* act, const float* c_all, const float* cm, const float* keep, const float* w_hh_t,
                      const float* dhid, const float* dhT, const float* dcT, int32_t T, int32_t B, int32_t H,
                      float* dgates, float* dh0, float* dc0, void* stream);
+
+/* Gradient-norm clipping + Adam over one network's parameter tensors in two launches (RPO-LSTM/agent.py:124-134:
+ * nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step(); torch/optim/adam.py single-tensor order).
+ * The table lists up to OUZ_ADAM_MAX_TENSORS f32 tensors (contiguous, numel elements each): gradient (read only),
+ * parameter, exp_avg and exp_avg_sq (updated in place).  step: the Adam step count after this step (1, 2, ...);
+ * max_norm <= 0: no clipping.  workspace: 256 floats of device memory. */
+#define OUZ_ADAM_MAX_TENSORS 16
+typedef struct ouz_adam_table {
+  int32_t n_tensors;
+  int32_t reserved;
+  int64_t numel[OUZ_ADAM_MAX_TENSORS];
+  const float* grad[OUZ_ADAM_MAX_TENSORS];
+  float* param[OUZ_ADAM_MAX_TENSORS];
+  float* exp_avg[OUZ_ADAM_MAX_TENSORS];
+  float* exp_avg_sq[OUZ_ADAM_MAX_TENSORS];
+} ouz_adam_table;
+int ouz_adam_clip_step(const ouz_adam_table* t, double lr, double beta1, double beta2, double eps, int64_t step,
+                       double max_norm, float* workspace, void* stream);
 
 /* PPO losses of one minibatch, forward + gradient for a unit upstream gradient in one call (the losses end the
  * graph).  Reductions are deterministic (fixed grid of OUZ_LOSS_BLOCKS per-block f64 partials summed in order).

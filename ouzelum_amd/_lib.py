@@ -91,6 +91,16 @@ class OuzTaskInfo(ctypes.Structure):
                 ("target_mode", ctypes.c_int32), ("plat_offset_x", ctypes.c_float)]
 
 
+ADAM_MAX_TENSORS = 16   # OUZ_ADAM_MAX_TENSORS
+
+
+class OuzAdamTable(ctypes.Structure):
+    _fields_ = [("n_tensors", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("numel", ctypes.c_int64 * ADAM_MAX_TENSORS), ("grad", ctypes.c_void_p * ADAM_MAX_TENSORS),
+                ("param", ctypes.c_void_p * ADAM_MAX_TENSORS), ("exp_avg", ctypes.c_void_p * ADAM_MAX_TENSORS),
+                ("exp_avg_sq", ctypes.c_void_p * ADAM_MAX_TENSORS)]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int32
 _F = ctypes.c_float
@@ -150,6 +160,8 @@ SIGNATURES = {
     "ouz_ppo_value_loss": (_I, [_P, _P, _I, _P, _P, _P, _P]),
     "ouz_tanh_bwd_bias": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "ouz_policy_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "ouz_adam_clip_step": (_I, [ctypes.POINTER(OuzAdamTable), ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                ctypes.c_double, _I64, ctypes.c_double, _P, _P]),
 }
 LOSS_WS_DOUBLES = 10 * 256      # OUZ_LOSS_WS_DOUBLES
 COLSUM_BLOCKS = 1024            # OUZ_COLSUM_BLOCKS

@@ -10,6 +10,8 @@
 //    of a CPU torch.rand coin + a CPU noise tensor copied H2D every step.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/ouzelum.h"
@@ -404,13 +406,17 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(const float* __restr
 // depends on that row only, so each workgroup owns 16 batch rows for all T steps and needs no grid
 // synchronisation: the carry stays on chip (c in registers, the masked h in LDS as the next step's MFMA operand)
 // instead of 2 launches + 4 B x H round trips per step.  The recurrent product runs on the f32 MFMA
-// (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulation); W_hh (256 KB) is read from L2 each step.
-//   wave w of the workgroup owns hidden units [32 w, 32 w + 32): two 16-column blocks jb, and for each the four
-//   gate tiles (columns q H + 32 w + 16 jb + [0, 16), q = i, f, g, o), so a lane's accumulators hold all four gates
-//   of its (row, unit) elements and the cell update needs no data movement.  MFMA C / D map: lane l holds rows
-//   4 (l >> 4) + r (r = 0..3) of column l & 15.  The K loop visits k in the order 16 p + 4 (l >> 4) + s
-//   (p: 16-wide slab, s = 0..3 the MFMA's step), so every lane's operands of four consecutive steps are one
-//   16-byte load (LDS for the carry / gradient tile, global for the weights).
+// (v_mfma_f32_16x16x4_f32, exact f32 products, f32 accumulation).
+//   wave w of the workgroup owns hidden units [32 w, 32 w + 32): two 16-unit blocks jb, and for each the four
+//   gate tiles (gate rows q H + 32 w + 16 jb + [0, 16), q = i, f, g, o), so a lane's accumulators hold all four gates
+//   of its (row, unit) elements and the cell update needs no data movement.  The product is computed transposed,
+//   gates^T = W_hh h^T (the weight fragment is the MFMA's A operand, the carry tile its B operand), so that with the
+//   MFMA's C / D map (lane l holds rows 4 (l >> 4) + r, r = 0..3, of column l & 15) a lane holds FOUR CONSECUTIVE
+//   hidden units of ONE batch row: every global load and store of a step is one 16-byte access per lane (a
+//   16-row x 64-byte block per instruction), 4x fewer memory instructions than the untransposed map, whose lanes
+//   held one unit of four rows.  The K loop visits k in the order 16 p + 4 (l >> 4) + s (p: 16-wide slab, s = 0..3
+//   the MFMA's step), so every lane's operands of four consecutive steps are one 16-byte load (LDS for the carry /
+//   gradient tile, registers for the weights).
 // ---------------------------------------------------------------------------
 constexpr int kSeqH = 128;
 constexpr int kSeqG = 4 * kSeqH;
@@ -423,267 +429,316 @@ __device__ __forceinline__ f32x4 mfma4(f32x4 a, f32x4 b, f32x4 c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, c, 0, 0, 0);
 }
+// The cell's transcendentals in the sequence kernels from the hardware's exp2 / reciprocal (v_exp_f32, v_rcp_f32,
+// ~1 ulp each): 4 and 7 instructions against ~12 and ~30 for the libm forms the per-step cell kernels keep.  sigmoid
+// to ~3 ulp; tanh to ~1e-7 absolute (1 - t loses the relative precision of tanh near 0, not its absolute one).
+__device__ __forceinline__ float fsigm(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float ftanh(float x) {
+  const float t = __builtin_amdgcn_exp2f(-2.88539008177792681f * fabsf(x));   // exp(-2|x|) in (0, 1]
+  return copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), x);
+}
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
 // Forward over T steps.  x_proj [T][B][4H] = x W_ih^T + b (pre-activation without the recurrent term), h0 / c0 [B][H],
 // keep [T][B] (1 - done: zeroes the carry entering step t), w [4H][H] (W_hh).  Writes, as the per-step path does,
 // act [T][B][4H] (activated gates), c_all / hid [T][B][H] and the masked carries hm / cm [T + 1][B][H] entering each
-// step (row T: the final carry, or h_out / c_out when given).  act, c_all, hm, cm may be null (inference).
-__global__ void __launch_bounds__(256) lstm_seq_fwd_kernel(
-    const float* __restrict__ xp, const float* h0, const float* c0, const float* __restrict__ keep,
-    const float* __restrict__ w, int T, int B, float* __restrict__ act, float* __restrict__ c_all,
-    float* __restrict__ hid, float* __restrict__ hm, float* __restrict__ cm, float* h_out, float* c_out) {
+// step (row T: the final carry, or h_out / c_out when given).  act, c_all, hm, cm may be null (inference).  Every
+// [.][B][.] buffer is 16-byte aligned (ouz_lstm_seq_fwd checks).
+// FULL: all 16 rows of the workgroup are valid (every workgroup but a ragged last one), so no load or store is
+// predicated.  SAVED: act / c_all / hm / cm are written (training; all four or none).  With a fixed number of stores
+// per step, the waitcnt pass can wait for a prefetched input with vmcnt(stores issued since) instead of vmcnt(0),
+// which drained the step's stores before the next step could start.
+template <int NJB, bool FULL, bool SAVED>
+__device__ __forceinline__ void lstm_seq_fwd_body(
+    float (*sh)[kSeqRows][kSeqH + 4], const float* __restrict__ xp, const float* h0, const float* c0,
+    const float* __restrict__ keep, const float* __restrict__ w, int T, int B, float* __restrict__ act,
+    float* __restrict__ c_all, float* __restrict__ hid, float* __restrict__ hm, float* __restrict__ cm, float* h_out,
+    float* c_out) {
   // (h_out / c_out may alias h0 / c0: each workgroup reads its rows of h0 / c0 first and writes the same rows last)
-  // the masked h entering the step (the MFMA's A operand), double-buffered by step parity so that a wave's cell
-  // update of one column block can run beside its MFMAs of the other (rows padded: conflict-free)
-  __shared__ float sh[2][kSeqRows][kSeqH + 4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
   const int r0 = blockIdx.x * kSeqRows;
-  for (int e = threadIdx.x; e < kSeqRows * kSeqH; e += 256) {
+  for (int e = threadIdx.x; e < kSeqRows * kSeqH; e += 512 / NJB) {
     const int row = e / kSeqH, j = e - row * kSeqH, b = r0 + row;
     const float v = b < B ? h0[(size_t)b * kSeqH + j] * keep[b] : 0.0f;
     sh[0][row][j] = v;
-    if (hm && b < B) hm[(size_t)b * kSeqH + j] = v;
+    if (SAVED && b < B) hm[(size_t)b * kSeqH + j] = v;
   }
-  float c[2][4];
+  // this lane's batch row (a ragged last workgroup computes zero rows and stores nothing for them) and its units
+  // j0[jb] + 0..3 of each block
+  const int b = r0 + li;
+  const bool bv = FULL || b < B;
+  int j0[NJB];
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb)
+  for (int jb = 0; jb < NJB; ++jb) j0[jb] = 16 * (NJB * wv + jb) + 4 * lg;
+  f32x4 c[NJB];
+  {
+    const float k0 = bv ? keep[b] : 0.0f;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = r0 + 4 * lg + r, j = 32 * wv + 16 * jb + li;
-      c[jb][r] = b < B ? c0[(size_t)b * kSeqH + j] * keep[b] : 0.0f;
-      if (cm && b < B) cm[(size_t)b * kSeqH + j] = c[jb][r];
+    for (int jb = 0; jb < NJB; ++jb) {
+      c[jb] = bv ? ld4(c0 + (size_t)b * kSeqH + j0[jb]) * k0 : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (SAVED && bv) st4(cm + (size_t)b * kSeqH + j0[jb], c[jb]);
     }
+  }
   // the wave's weight fragments, packed by ouz_lstm_seq_pack in the order the lanes consume them (wf [wave][slab]
   // [jb][q][lane] f32x4): every fragment load is one contiguous 1 KB (eight full cache lines) per wave.
-  // The wave's whole weight slice (128 gate columns x 128, 64 KB: 256 registers per lane) is loaded once and kept in
+  // The wave's whole weight slice (128 gate rows x 128, 64 KB: 256 registers per lane) is loaded once and kept in
   // registers for all T steps (one wave per SIMD: the register file has room), so the steps read no weights at all.
-  const f32x4* wl = reinterpret_cast<const f32x4*>(w) + (size_t)wv * (kSeqH / 16) * 8 * 64 + lane;
-  f32x4 wreg[kSeqH / 16][2][4];
+  // (block gb = NJB wv + jb of the eight 16-unit blocks sits at wf[gb >> 1][.][gb & 1])
+  const f32x4* wl = reinterpret_cast<const f32x4*>(w) + lane;
+  f32x4 wreg[kSeqH / 16][NJB][4];
 #pragma unroll
   for (int p = 0; p < kSeqH / 16; ++p)
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
+    for (int jb = 0; jb < NJB; ++jb) {
+      const int gb = NJB * wv + jb;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wreg[p][jb][q] = wl[((size_t)p * 8 + jb * 4 + q) * 64];
-  // this lane's rows and their validity (a ragged last workgroup computes zero rows and stores nothing for them)
-  int rb[4];
-  bool rv[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    rb[r] = r0 + 4 * lg + r;
-    rv[r] = rb[r] < B;
-  }
+      for (int q = 0; q < 4; ++q) wreg[p][jb][q] = wl[((((size_t)(gb >> 1) * 8 + p) * 2 + (gb & 1)) * 4 + q) * 64];
+    }
   // A step's inputs (its input projection, the next step's keep) are loaded one step ahead, before the previous
   // step's output stores: gfx950's single vmcnt counter retires loads and stores in order, so loads issued after
-  // a step's 64 stores could not be waited for without waiting for those stores too (SQ_WAIT_INST_ANY was 41 %
-  // of the wave's cycles with the loads at the top of the step).
-  float x[2][4][4], kn[4], xn[2][4][4], knn[4];
-  const auto load_inputs = [&](int t, float (&xd)[2][4][4], float (&kd)[4]) {
+  // a step's stores could not be waited for without waiting for those stores too.  The inputs alternate between two
+  // register sets (the loop runs two steps per trip): with one set, the hand-over of the prefetched keep to the next
+  // step was a register copy, and that copy's s_waitcnt vmcnt(0) drained every store of the step before the next
+  // one could start.
+  f32x4 xa[NJB][4], xb[NJB][4];
+  float ka, kb;
+  const auto load_inputs = [&](int t, f32x4 (&xd)[NJB][4], float& kd) {
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
+    for (int jb = 0; jb < NJB; ++jb)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          xd[jb][q][r] = rv[r] ? xp[((size_t)t * B + rb[r]) * kSeqG + q * kSeqH + 32 * wv + 16 * jb + li] : 0.0f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kd[r] = (t + 1 < T && rv[r]) ? keep[(size_t)(t + 1) * B + rb[r]] : 1.0f;
+        xd[jb][q] = bv ? ld4(xp + ((size_t)t * B + b) * kSeqG + q * kSeqH + j0[jb]) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    kd = (t + 1 < T && bv) ? keep[(size_t)(t + 1) * B + b] : 1.0f;
   };
-  load_inputs(0, x, kn);
-  for (int t = 0; t < T; ++t) {
+  const auto step = [&](int t, const f32x4 (&x)[NJB][4], float kn, f32x4 (&xn)[NJB][4], float& knn) {
     const int cur = t & 1;
     const bool last = t == T - 1;
     __syncthreads();   // sh[cur] holds this step's carry (and every wave is done with sh[cur ^ 1])
-    float ig[2][4], fg[2][4], gg[2][4], og[2][4], cn[2][4], hn[2][4];
+    f32x4 ig[NJB], fg[NJB], gg[NJB], og[NJB], cn[NJB], hn[NJB], hv[NJB];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      // the product of column block jb; block 0's cell update below is independent of block 1's MFMAs, so the
+    for (int jb = 0; jb < NJB; ++jb) {
+      // the product of unit block jb; block 0's cell update below is independent of block 1's MFMAs, so the
       // scheduler can issue its VALU work while those run
       f32x4 acc[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int p = 0; p < kSeqH / 16; ++p) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(&sh[cur][li][16 * p + 4 * lg]);
+        const f32x4 h = ld4(&sh[cur][li][16 * p + 4 * lg]);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = mfma4(a, wreg[p][jb][q], acc[q]);
+        for (int q = 0; q < 4; ++q) acc[q] = mfma4(wreg[p][jb][q], h, acc[q]);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         // gates = x_proj + h W_hh^T (the GEMM path's beta = 1 accumulation: the projection added to the product)
-        ig[jb][r] = sigm(x[jb][0][r] + acc[0][r]);
-        fg[jb][r] = sigm(x[jb][1][r] + acc[1][r]);
-        gg[jb][r] = tanhf(x[jb][2][r] + acc[2][r]);
-        og[jb][r] = sigm(x[jb][3][r] + acc[3][r]);
+        ig[jb][r] = fsigm(x[jb][0][r] + acc[0][r]);
+        fg[jb][r] = fsigm(x[jb][1][r] + acc[1][r]);
+        gg[jb][r] = ftanh(x[jb][2][r] + acc[2][r]);
+        og[jb][r] = fsigm(x[jb][3][r] + acc[3][r]);
         cn[jb][r] = fg[jb][r] * c[jb][r] + ig[jb][r] * gg[jb][r];
-        hn[jb][r] = og[jb][r] * tanhf(cn[jb][r]);
-        const float hmv = kn[r] * hn[jb][r];
-        c[jb][r] = kn[r] * cn[jb][r];
-        sh[cur ^ 1][4 * lg + r][32 * wv + 16 * jb + li] = hmv;
+        hn[jb][r] = og[jb][r] * ftanh(cn[jb][r]);
+        hv[jb][r] = kn * hn[jb][r];   // the masked carry: the next step's operand (LDS) and hm / h_out
+        c[jb][r] = kn * cn[jb][r];
       }
+      st4(&sh[cur ^ 1][li][j0[jb]], hv[jb]);
     }
     if (!last) load_inputs(t + 1, xn, knn);   // ahead of this step's stores
-    float knc[4];
+    if (bv) {
+      const size_t base = (size_t)t * B + b;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) knc[r] = kn[r];
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!rv[r]) continue;
-        const int b = rb[r], j = 32 * wv + 16 * jb + li;
-        const size_t base = (size_t)t * B + b;
-        if (act) {
-          float* a = act + base * kSeqG;
-          a[j] = ig[jb][r]; a[kSeqH + j] = fg[jb][r]; a[2 * kSeqH + j] = gg[jb][r]; a[3 * kSeqH + j] = og[jb][r];
+      for (int jb = 0; jb < NJB; ++jb) {
+        if (SAVED) {
+          float* a = act + base * kSeqG + j0[jb];
+          st4(a, ig[jb]); st4(a + kSeqH, fg[jb]); st4(a + 2 * kSeqH, gg[jb]); st4(a + 3 * kSeqH, og[jb]);
         }
-        if (c_all) c_all[base * kSeqH + j] = cn[jb][r];
-        hid[base * kSeqH + j] = hn[jb][r];
-        const float hmv = knc[r] * hn[jb][r];
+        if (SAVED) st4(c_all + base * kSeqH + j0[jb], cn[jb]);
+        st4(hid + base * kSeqH + j0[jb], hn[jb]);
         if (last && h_out) {
-          h_out[(size_t)b * kSeqH + j] = hmv;
-          c_out[(size_t)b * kSeqH + j] = c[jb][r];
+          st4(h_out + (size_t)b * kSeqH + j0[jb], hv[jb]);
+          st4(c_out + (size_t)b * kSeqH + j0[jb], c[jb]);
         } else {
-          const size_t nx = ((size_t)(t + 1) * B + b) * kSeqH + j;
-          if (hm) hm[nx] = hmv;
-          if (cm) cm[nx] = c[jb][r];
+          const size_t nx = ((size_t)(t + 1) * B + b) * kSeqH + j0[jb];
+          if (SAVED) {
+            st4(hm + nx, hv[jb]);
+            st4(cm + nx, c[jb]);
+          }
         }
       }
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) x[jb][q][r] = xn[jb][q][r];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kn[r] = knn[r];
+    }
+  };
+  // the weight loads complete here, once: otherwise the waitcnt pass, merging the loop's entry state (32 fragment
+  // loads in flight) into its header, put an s_waitcnt vmcnt(0) before the first MFMA on each fragment in EVERY step,
+  // draining the previous step's stores too
+  __builtin_amdgcn_s_waitcnt(0);
+  // step 0 is peeled so that the loop is entered, like its back edge, right after a step's prefetch and stores:
+  // the waitcnt pass merges both into the loop header, and an entry straight after load_inputs(0) would make the
+  // loop's first wait for the inputs a vmcnt(0) on every trip
+  load_inputs(0, xa, ka);
+  step(0, xa, ka, xb, kb);
+  int t = 1;
+  for (; t + 1 < T; t += 2) {
+    step(t, xb, kb, xa, ka);
+    step(t + 1, xa, ka, xb, kb);
   }
+  if (t < T) step(t, xb, kb, xa, ka);
+}
+
+template <int NJB, bool SAVED>
+__global__ void __launch_bounds__(512 / NJB) lstm_seq_fwd_kernel(
+    const float* __restrict__ xp, const float* h0, const float* c0, const float* __restrict__ keep,
+    const float* __restrict__ w, int T, int B, float* __restrict__ act, float* __restrict__ c_all,
+    float* __restrict__ hid, float* __restrict__ hm, float* __restrict__ cm, float* h_out, float* c_out) {
+  // the masked h entering the step (the MFMA's B operand), double-buffered by step parity so that a wave's cell
+  // update can run beside the MFMAs of the next unit block (rows padded: conflict-free)
+  __shared__ float sh[2][kSeqRows][kSeqH + 4];
+  if ((int)(blockIdx.x + 1) * kSeqRows <= B)
+    lstm_seq_fwd_body<NJB, true, SAVED>(sh, xp, h0, c0, keep, w, T, B, act, c_all, hid, hm, cm, h_out, c_out);
+  else
+    lstm_seq_fwd_body<NJB, false, SAVED>(sh, xp, h0, c0, keep, w, T, B, act, c_all, hid, hm, cm, h_out, c_out);
 }
 
 // BPTT over T steps (the mirror of lstm_seq_fwd_kernel and of the per-step lstm_cell_bwd_kernel + GEMM): per step
 // dh = dhid + keep_{t+1} G with G = dgates_{t+1} W_hh (the MFMA product, K = 4H, from the dgates tile kept in LDS;
 // at t = T - 1 G is dhT, or nothing), dc = keep_{t+1} dc_next + dh o (1 - tanh(c)^2).  Writes dgates [T][B][4H]
-// (pre-activation), dh0 = (dgates_0 W_hh) keep_0 and dc0 = dc keep_0 [B][H].  wt = W_hh^T [H][4H] (contiguous), so
-// the weight fragments are 16-byte loads along k.
-__global__ void __launch_bounds__(256) lstm_seq_bwd_kernel(
-    const float* __restrict__ act, const float* __restrict__ c_all, const float* __restrict__ cm,
-    const float* __restrict__ keep, const float* __restrict__ wt, const float* __restrict__ dhid,
-    const float* __restrict__ dhT, const float* __restrict__ dcT, int T, int B, float* __restrict__ dgates,
-    float* __restrict__ dh0, float* __restrict__ dc0) {
-  // dgates of the step after (A operand of G), double-buffered by step parity: a wave's cell update of one column
-  // block runs beside its MFMAs of the other, one barrier per step
-  __shared__ float sg[2][kSeqRows][kSeqG + 4];
+// (pre-activation), dh0 = (dgates_0 W_hh) keep_0 and dc0 = dc keep_0 [B][H].  Same transposed product and lane map
+// as the forward (G^T = W_hh^T dgates^T: a lane holds four consecutive units of one row).
+template <int NJB, bool FULL>
+__device__ __forceinline__ void lstm_seq_bwd_body(
+    float (*sg)[kSeqRows][kSeqG + 4], const float* __restrict__ act, const float* __restrict__ c_all,
+    const float* __restrict__ cm, const float* __restrict__ keep, const float* __restrict__ wt,
+    const float* __restrict__ dhid, const float* __restrict__ dhT, const float* __restrict__ dcT, int T, int B,
+    float* __restrict__ dgates, float* __restrict__ dh0, float* __restrict__ dc0) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, lg = lane >> 4;
   const int r0 = blockIdx.x * kSeqRows;
-  // packed W_hh^T fragments (ouz_lstm_seq_pack: wb [wave][slab][jb][lane] f32x4, one contiguous 1 KB per load): the
+  // packed W_hh fragments (ouz_lstm_seq_pack: wb [wave][slab][jb][lane] f32x4, one contiguous 1 KB per load): the
   // wave's slice (32 hidden units x 512 gate columns, 64 KB: 256 registers per lane) is loaded once for all T steps
-  const f32x4* wl = reinterpret_cast<const f32x4*>(wt) + (size_t)wv * (kSeqG / 16) * 2 * 64 + lane;
-  f32x4 wreg[kSeqG / 16][2];
+  // (block gb = NJB wv + jb of the eight 16-unit blocks sits at wb[gb >> 1][.][gb & 1])
+  const f32x4* wl = reinterpret_cast<const f32x4*>(wt) + lane;
+  f32x4 wreg[kSeqG / 16][NJB];
 #pragma unroll
-  for (int p = 0; p < kSeqG / 16; ++p) {
-    wreg[p][0] = wl[(size_t)p * 128];
-    wreg[p][1] = wl[(size_t)p * 128 + 64];
-  }
-  // G of column block jb = sg[buf] W_hh over the 4H gate columns
+  for (int p = 0; p < kSeqG / 16; ++p)
+#pragma unroll
+    for (int jb = 0; jb < NJB; ++jb) {
+      const int gb = NJB * wv + jb;
+      wreg[p][jb] = wl[(((size_t)(gb >> 1) * 32 + p) * 2 + (gb & 1)) * 64];
+    }
+  // G of unit block jb (transposed: lane holds units j0[jb] + 0..3 of row li) = sg[buf] W_hh over the 4H gates
   const auto product = [&](int buf, int jb) {
     f32x4 acc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int p = 0; p < kSeqG / 16; ++p) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(&sg[buf][li][16 * p + 4 * lg]);
-      acc = mfma4(a, wreg[p][jb], acc);
-    }
+    for (int p = 0; p < kSeqG / 16; ++p) acc = mfma4(wreg[p][jb], ld4(&sg[buf][li][16 * p + 4 * lg]), acc);
     return acc;
   };
-  int rb[4];
-  bool rv[4];
+  const int b = r0 + li;
+  const bool bv = FULL || b < B;
+  int j0[NJB];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    rb[r] = r0 + 4 * lg + r;
-    rv[r] = rb[r] < B;
-  }
-  float dc[2][4];
+  for (int jb = 0; jb < NJB; ++jb) j0[jb] = 16 * (NJB * wv + jb) + 4 * lg;
+  const f32x4 zero4 = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 dc[NJB];
   // the cell's saved values of a step are loaded one step ahead, before the later step's dgates stores (one
   // in-order vmcnt counter for loads and stores: see lstm_seq_fwd_kernel)
-  float ag[2][4][4], cv[2][4], cp[2][4], dy[2][4], kn[4];
-  const auto load_saved = [&](int t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) kn[r] = (t + 1 < T && rv[r]) ? keep[(size_t)(t + 1) * B + rb[r]] : 1.0f;
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 32 * wv + 16 * jb + li;
-        const size_t base = (size_t)t * B + rb[r];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ag[jb][q][r] = rv[r] ? act[base * kSeqG + q * kSeqH + j] : 0.0f;
-        cv[jb][r] = rv[r] ? c_all[base * kSeqH + j] : 0.0f;
-        cp[jb][r] = rv[r] ? cm[base * kSeqH + j] : 0.0f;
-        dy[jb][r] = rv[r] ? dhid[base * kSeqH + j] : 0.0f;
-      }
+  // (two register sets, alternating by step: see lstm_seq_fwd_kernel)
+  struct Saved {
+    f32x4 ag[NJB][4], cv[NJB], cp[NJB], dy[NJB];
+    float kn;
   };
-  load_saved(T - 1);
-  for (int t = T - 1; t >= 0; --t) {
+  Saved sa, sb;
+  const auto load_saved = [&](int t, Saved& sv) {
+    sv.kn = (t + 1 < T && bv) ? keep[(size_t)(t + 1) * B + b] : 1.0f;
+    const size_t base = (size_t)t * B + b;
+#pragma unroll
+    for (int jb = 0; jb < NJB; ++jb) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sv.ag[jb][q] = bv ? ld4(act + base * kSeqG + q * kSeqH + j0[jb]) : zero4;
+      sv.cv[jb] = bv ? ld4(c_all + base * kSeqH + j0[jb]) : zero4;
+      sv.cp[jb] = bv ? ld4(cm + base * kSeqH + j0[jb]) : zero4;
+      sv.dy[jb] = bv ? ld4(dhid + base * kSeqH + j0[jb]) : zero4;
+    }
+  };
+  const auto step = [&](int t, const Saved& sv, Saved& nx) {
+    const auto& ag = sv.ag;
+    const auto& cv = sv.cv;
+    const auto& cp = sv.cp;
+    const auto& dy = sv.dy;
+    const float kn = sv.kn;
     const bool lastt = t == T - 1;
     const int cur = t & 1;   // the buffer this step writes; it reads cur ^ 1 (written by step t + 1)
     const bool has_g = !lastt || dhT != nullptr;
     const bool has_dc = !lastt || dcT != nullptr;
     // sg[cur ^ 1] holds dgates_{t+1}, and every wave is done with sg[cur] (read by step t + 1)
     if (!lastt) __syncthreads();
-    float di[2][4], df[2][4], dg[2][4], d_o[2][4];
+    f32x4 di[NJB], df[NJB], dg[NJB], d_o[NJB];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) {
-      f32x4 acc;
+    for (int jb = 0; jb < NJB; ++jb) {
+      f32x4 acc, dcn;
       if (lastt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          acc[r] = (dhT && rv[r]) ? dhT[(size_t)rb[r] * kSeqH + 32 * wv + 16 * jb + li] : 0.0f;
+        acc = (dhT && bv) ? ld4(dhT + (size_t)b * kSeqH + j0[jb]) : zero4;
+        dcn = (dcT && bv) ? ld4(dcT + (size_t)b * kSeqH + j0[jb]) : zero4;
       } else {
         acc = product(cur ^ 1, jb);
+        dcn = dc[jb];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int j = 32 * wv + 16 * jb + li;
-        const float k = kn[r];
-        const float dcn = lastt ? ((dcT && rv[r]) ? dcT[(size_t)rb[r] * kSeqH + j] : 0.0f) : dc[jb][r];
-        const float dh = dy[jb][r] + (has_g ? k * acc[r] : 0.0f);
+        const float dh = dy[jb][r] + (has_g ? kn * acc[r] : 0.0f);
         const float ig = ag[jb][0][r], fg = ag[jb][1][r], gg = ag[jb][2][r], og = ag[jb][3][r];
-        const float tc = tanhf(cv[jb][r]);
-        const float dcv = (has_dc ? k * dcn : 0.0f) + dh * og * (1.0f - tc * tc);
+        const float tc = ftanh(cv[jb][r]);
+        const float dcv = (has_dc ? kn * dcn[r] : 0.0f) + dh * og * (1.0f - tc * tc);
         di[jb][r] = dcv * gg * ig * (1.0f - ig);
         df[jb][r] = dcv * cp[jb][r] * fg * (1.0f - fg);
         dg[jb][r] = dcv * ig * (1.0f - gg * gg);
         d_o[jb][r] = dh * tc * og * (1.0f - og);
-        float* srow = sg[cur][4 * lg + r];
-        srow[j] = di[jb][r]; srow[kSeqH + j] = df[jb][r]; srow[2 * kSeqH + j] = dg[jb][r];
-        srow[3 * kSeqH + j] = d_o[jb][r];
         dc[jb][r] = dcv * fg;
       }
+      float* srow = &sg[cur][li][j0[jb]];
+      st4(srow, di[jb]); st4(srow + kSeqH, df[jb]); st4(srow + 2 * kSeqH, dg[jb]); st4(srow + 3 * kSeqH, d_o[jb]);
     }
-    if (t > 0) load_saved(t - 1);   // ahead of this step's stores (the values above are consumed)
+    if (t > 0) load_saved(t - 1, nx);   // ahead of this step's stores
+    if (bv) {
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (!rv[r]) continue;
-        const int j = 32 * wv + 16 * jb + li;
-        float* d = dgates + ((size_t)t * B + rb[r]) * kSeqG;
-        d[j] = di[jb][r]; d[kSeqH + j] = df[jb][r]; d[2 * kSeqH + j] = dg[jb][r]; d[3 * kSeqH + j] = d_o[jb][r];
+      for (int jb = 0; jb < NJB; ++jb) {
+        float* d = dgates + ((size_t)t * B + b) * kSeqG + j0[jb];
+        st4(d, di[jb]); st4(d + kSeqH, df[jb]); st4(d + 2 * kSeqH, dg[jb]); st4(d + 3 * kSeqH, d_o[jb]);
       }
+    }
+  };
+  __builtin_amdgcn_s_waitcnt(0);   // the weight loads complete once, before the loop (see lstm_seq_fwd_kernel)
+  load_saved(T - 1, sa);
+  step(T - 1, sa, sb);   // peeled, as in lstm_seq_fwd_kernel
+  int t = T - 2;
+  for (; t >= 1; t -= 2) {
+    step(t, sb, sa);
+    step(t - 1, sa, sb);
   }
+  if (t == 0) step(0, sb, sa);
   // dh0 = (dgates_0 W_hh) keep_0, dc0 = dc keep_0
   __syncthreads();
 #pragma unroll
-  for (int jb = 0; jb < 2; ++jb) {
+  for (int jb = 0; jb < NJB; ++jb) {
     const f32x4 acc = product(0, jb);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (!rv[r]) continue;
-      const int j = 32 * wv + 16 * jb + li;
-      const float k0 = keep[rb[r]];
-      if (dh0) dh0[(size_t)rb[r] * kSeqH + j] = acc[r] * k0;
-      if (dc0) dc0[(size_t)rb[r] * kSeqH + j] = dc[jb][r] * k0;
-    }
+    if (!bv) continue;
+    const float k0 = keep[b];
+    if (dh0) st4(dh0 + (size_t)b * kSeqH + j0[jb], acc * k0);
+    if (dc0) st4(dc0 + (size_t)b * kSeqH + j0[jb], dc[jb] * k0);
   }
+}
+
+template <int NJB>
+__global__ void __launch_bounds__(512 / NJB) lstm_seq_bwd_kernel(
+    const float* __restrict__ act, const float* __restrict__ c_all, const float* __restrict__ cm,
+    const float* __restrict__ keep, const float* __restrict__ wt, const float* __restrict__ dhid,
+    const float* __restrict__ dhT, const float* __restrict__ dcT, int T, int B, float* __restrict__ dgates,
+    float* __restrict__ dh0, float* __restrict__ dc0) {
+  // dgates of the step after (B operand of G), double-buffered by step parity: one barrier per step
+  __shared__ float sg[2][kSeqRows][kSeqG + 4];
+  if ((int)(blockIdx.x + 1) * kSeqRows <= B)
+    lstm_seq_bwd_body<NJB, true>(sg, act, c_all, cm, keep, wt, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
+  else
+    lstm_seq_bwd_body<NJB, false>(sg, act, c_all, cm, keep, wt, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
 }
 
 // The weight fragments of lstm_seq_fwd_kernel / lstm_seq_bwd_kernel in consumption order (one thread per f32x4):
@@ -712,6 +767,70 @@ int launch_status(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(OUZ_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
   return OUZ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Gradient-norm clipping + Adam over one network's parameters in two launches (RPO-LSTM/agent.py:124-134:
+// nn.utils.clip_grad_norm_(parameters, max_grad_norm) then optim.Adam.step()), in place of torch's per-tensor norms,
+// their stack / norm / clamp / scale launches and the multi-tensor Adam kernel (~6 launches and ~70 us per step on a
+// < 1 M-parameter network: the multi-tensor kernel's grid is sized by tensor chunks, not by the chip).
+//   adam_sqnorm_kernel: kAdamBlocks partial sums of g^2 over every tensor of the table (grid-stride, fixed order);
+//   adam_step_kernel: every block reduces the same partials in the same order (so all agree on the norm without a
+//   third launch), clip coefficient min(max_norm / (||g|| + 1e-6), 1) as torch computes it, then the Adam update in
+//   torch's single-tensor order (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, denom = sqrt(v) / sqrt(bc2) + eps,
+//   param.addcdiv_(m, denom, -lr / bc1)).  The clipped gradient is not written back (nothing reads it after step).
+// ---------------------------------------------------------------------------
+constexpr int kAdamBlocks = 256;
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ void __launch_bounds__(256) adam_sqnorm_kernel(ouz_adam_table t, float* __restrict__ part) {
+  __shared__ float red[256];
+  const int64_t stride = (int64_t)gridDim.x * 256, g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float acc = 0.0f;
+  for (int i = 0; i < t.n_tensors; ++i) {
+    const float* g = t.grad[i];
+    for (int64_t e = g0; e < t.numel[i]; e += stride) acc += g[e] * g[e];
+  }
+  const float s = block_sum256(acc, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ void __launch_bounds__(256) adam_step_kernel(ouz_adam_table t, const float* __restrict__ part, float lr_bc1,
+                                                        float w1, float beta2, float w2, float eps, float bc2_sqrt,
+                                                        float max_norm) {
+  __shared__ float red[256];
+  float coef = 1.0f;
+  if (max_norm > 0.0f) {
+    const float total = sqrtf(block_sum256(part[threadIdx.x], red));
+    coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+  }
+  const int64_t stride = (int64_t)gridDim.x * 256, g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (int i = 0; i < t.n_tensors; ++i) {
+    const float* g = t.grad[i];
+    float* p = t.param[i];
+    float* m = t.exp_avg[i];
+    float* v = t.exp_avg_sq[i];
+    for (int64_t e = g0; e < t.numel[i]; e += stride) {
+      const float gc = g[e] * coef;
+      const float mn = m[e] + w1 * (gc - m[e]);   // lerp(m, g, 1 - beta1)
+      const float vn = v[e] * beta2 + w2 * gc * gc;
+      m[e] = mn;
+      v[e] = vn;
+      p[e] = p[e] + (-lr_bc1) * (mn / (sqrtf(vn) / bc2_sqrt + eps));
+    }
+  }
 }
 
 }  // namespace
@@ -769,6 +888,17 @@ int ouz_lstm_cell_fwd(const float* gates, const float* c_prev_m, const float* ke
 
 static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Waves per workgroup of the sequence kernels: 8 (one 16-unit block per wave, two waves per SIMD: one wave's cell
+// update and stores run beside the other's MFMAs) or 4 (two blocks per wave, one wave per SIMD; 10-15 % slower,
+// profiles/r06/learn/lstm_seq_ab.txt); OUZ_LSTM_SEQ_WAVES=4 selects the latter.
+static int seq_waves() {
+  static const int w = [] {
+    const char* e = std::getenv("OUZ_LSTM_SEQ_WAVES");
+    return e && std::atoi(e) == 4 ? 4 : 8;
+  }();
+  return w;
+}
+
 int ouz_lstm_seq_pack(const float* w_hh, int32_t H, float* w_fwd, float* w_bwd, void* stream) {
   if (H != kSeqH) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_pack: H must be 128");
   if (!w_hh || !w_fwd || !w_bwd) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_pack: null buffer");
@@ -786,9 +916,23 @@ int ouz_lstm_seq_fwd(const float* x_proj, const float* h0, const float* c0, cons
   if (T <= 0 || B <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: T and B must be > 0");
   if (!x_proj || !h0 || !c0 || !keep || !w_hh || !hid || (!h_out) != (!c_out))
     return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: null buffer (h_out and c_out: both or neither)");
-  if (!aligned16(w_hh)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: w_fwd must be 16-byte aligned");
-  hipLaunchKernelGGL(lstm_seq_fwd_kernel, dim3(grid(B, kSeqRows)), dim3(256), 0, (hipStream_t)stream, x_proj, h0, c0,
-                     keep, w_hh, T, B, act, c_all, hid, hm, cm, h_out, c_out);
+  if ((!act) != (!c_all) || (!act) != (!hm) || (!act) != (!cm))
+    return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: act, c_all, hm and cm: all four or none");
+  for (const void* p : {(const void*)x_proj, (const void*)c0, (const void*)w_hh, (const void*)act, (const void*)c_all,
+                        (const void*)hid, (const void*)hm, (const void*)cm, (const void*)h_out, (const void*)c_out})
+    if (!aligned16(p)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_fwd: every buffer must be 16-byte aligned");
+  const dim3 g(grid(B, kSeqRows));
+  const hipStream_t s = (hipStream_t)stream;
+  const bool saved = act != nullptr;
+#define OUZ_SEQ_FWD(NJB, SAVED)                                                                                    \
+  hipLaunchKernelGGL((lstm_seq_fwd_kernel<NJB, SAVED>), g, dim3(512 / NJB), 0, s, x_proj, h0, c0, keep, w_hh, T, B, \
+                     act, c_all, hid, hm, cm, h_out, c_out)
+  if (seq_waves() == 8) {
+    if (saved) OUZ_SEQ_FWD(1, true); else OUZ_SEQ_FWD(1, false);
+  } else {
+    if (saved) OUZ_SEQ_FWD(2, true); else OUZ_SEQ_FWD(2, false);
+  }
+#undef OUZ_SEQ_FWD
   return launch_status("lstm_seq_fwd_kernel");
 }
 
@@ -799,9 +943,15 @@ int ouz_lstm_seq_bwd(const float* act, const float* c_all, const float* cm, cons
   if (T <= 0 || B <= 0) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: T and B must be > 0");
   if (!act || !c_all || !cm || !keep || !w_hh_t || !dhid || !dgates)
     return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: null buffer");
-  if (!aligned16(w_hh_t)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: w_bwd must be 16-byte aligned");
-  hipLaunchKernelGGL(lstm_seq_bwd_kernel, dim3(grid(B, kSeqRows)), dim3(256), 0, (hipStream_t)stream, act, c_all, cm,
-                     keep, w_hh_t, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
+  for (const void* p : {(const void*)act, (const void*)c_all, (const void*)cm, (const void*)w_hh_t, (const void*)dhid,
+                        (const void*)dhT, (const void*)dcT, (const void*)dgates, (const void*)dh0, (const void*)dc0})
+    if (!aligned16(p)) return set_error(OUZ_ERR_INVALID, "ouz_lstm_seq_bwd: every buffer must be 16-byte aligned");
+  if (seq_waves() == 8)
+    hipLaunchKernelGGL(lstm_seq_bwd_kernel<1>, dim3(grid(B, kSeqRows)), dim3(512), 0, (hipStream_t)stream, act, c_all,
+                       cm, keep, w_hh_t, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
+  else
+    hipLaunchKernelGGL(lstm_seq_bwd_kernel<2>, dim3(grid(B, kSeqRows)), dim3(256), 0, (hipStream_t)stream, act, c_all,
+                       cm, keep, w_hh_t, dhid, dhT, dcT, T, B, dgates, dh0, dc0);
   return launch_status("lstm_seq_bwd_kernel");
 }
 
@@ -871,6 +1021,26 @@ int ouz_policy_sample(const float* hidden, const float* w, const float* b, const
   hipLaunchKernelGGL(policy_sample_kernel, dim3(grid(B * OUZ_NUM_ACT, 256)), dim3(256), 0, (hipStream_t)stream, hidden,
                      w, b, logstd, eps, B, H, action, logprob, entropy);
   return launch_status("policy_sample_kernel");
+}
+
+
+int ouz_adam_clip_step(const ouz_adam_table* t, double lr, double beta1, double beta2, double eps, int64_t step,
+                       double max_norm, float* workspace, void* stream) {
+  if (!t || !workspace) return set_error(OUZ_ERR_INVALID, "ouz_adam_clip_step: null table or workspace");
+  if (t->n_tensors < 1 || t->n_tensors > OUZ_ADAM_MAX_TENSORS)
+    return set_error(OUZ_ERR_INVALID, "ouz_adam_clip_step: 1 to OUZ_ADAM_MAX_TENSORS tensors");
+  if (step < 1) return set_error(OUZ_ERR_INVALID, "ouz_adam_clip_step: step counts from 1");
+  for (int i = 0; i < t->n_tensors; ++i)
+    if (t->numel[i] < 0 || (t->numel[i] && (!t->grad[i] || !t->param[i] || !t->exp_avg[i] || !t->exp_avg_sq[i])))
+      return set_error(OUZ_ERR_INVALID, "ouz_adam_clip_step: null tensor in the table");
+  // torch's host-side scalars (Adam's non-capturable path): computed in double (Python floats), used as f32
+  const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+  const hipStream_t s = (hipStream_t)stream;
+  if (max_norm > 0.0) hipLaunchKernelGGL(adam_sqnorm_kernel, dim3(kAdamBlocks), dim3(256), 0, s, *t, workspace);
+  hipLaunchKernelGGL(adam_step_kernel, dim3(kAdamBlocks), dim3(256), 0, s, *t, workspace, (float)(lr / bc1),
+                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, (float)std::sqrt(bc2),
+                     (float)max_norm);
+  return launch_status("adam_step_kernel");
 }
 
 }  // extern "C"

@@ -220,12 +220,19 @@ def _p(t):
 SEQ_MIN_T = 4
 
 
-def seq_kernels_ok(x_proj):
+def seq_kernels_ok(x_proj, *bufs):
     """The fused sequence kernels apply: hidden size 128 (the reference actor's), f32, and a sequence of at least
     SEQ_MIN_T steps.  Each workgroup loads its 256 KB of weight fragments once per launch and keeps them in registers,
-    which pays over a sequence (the update's T = 16); the rollout's one-step policy calls keep the GEMM + cell pair."""
+    which pays over a sequence (the update's T = 16); the rollout's one-step policy calls keep the GEMM + cell pair.
+    ``bufs``: caller-owned output buffers (the in-place carry), which the kernels need 16-byte aligned."""
     return (_SEQ and x_proj.shape[-1] == 4 * SEQ_H and x_proj.dtype == torch.float32
-            and x_proj.shape[0] >= SEQ_MIN_T)
+            and x_proj.shape[0] >= SEQ_MIN_T and all(b.data_ptr() % 16 == 0 for b in bufs))
+
+
+def _a16(t):
+    """t, or an aligned copy: the sequence kernels make one 16-byte access per lane (a tensor that is a view at an
+    odd offset into a larger buffer is copied)."""
+    return t if t is None or t.data_ptr() % 16 == 0 else t.clone()
 
 
 def seq_pack(w_hh):
@@ -243,9 +250,9 @@ def _lstm_forward_seq(x_proj, h0, c0, keep, w_hh, carry_out=None, saved=True, pa
     T, B, G4 = x_proj.shape
     H = G4 // 4
     dev = x_proj.device
-    x_proj = x_proj.contiguous()
+    x_proj = _a16(x_proj.contiguous())
     keep = keep.contiguous().float()
-    h0, c0 = h0.contiguous(), c0.contiguous()
+    h0, c0 = h0.contiguous(), _a16(c0.contiguous())
     w = (packed or seq_pack(w_hh))[0]
     hid = torch.empty((T, B, H), device=dev)
     act = c_all = hm = cm = None
@@ -267,7 +274,7 @@ def _lstm_forward(x_proj, h0, c0, keep, w_hh, carry_out=None, saved=True):
     cm, keep).  ``carry_out=(h, c)``: the last step writes the final carry (keep = 1, so the masked next-step carry is
     the carry itself) into these buffers instead of the scratch row; they may alias h0 / c0, which are consumed
     (masked into hm[0] / cm[0]) before any cell launch."""
-    if seq_kernels_ok(x_proj):
+    if seq_kernels_ok(x_proj, *(carry_out or ())):
         return _lstm_forward_seq(x_proj, h0, c0, keep, w_hh, carry_out, saved)
     T, B, G4 = x_proj.shape
     H = G4 // 4
@@ -349,6 +356,7 @@ class LSTMSequence(torch.autograd.Function):
             ctx.packed_bwd = None
             dh0 = torch.empty((B, H), device=dev) if ctx.needs_input_grad[1] else None
             dc0 = torch.empty((B, H), device=dev) if ctx.needs_input_grad[2] else None
+            dhid, dhT, dcT = _a16(dhid), _a16(dhT), _a16(dcT)
             L.check(L.lib.ouz_lstm_seq_bwd(act.data_ptr(), c_all.data_ptr(), cm.data_ptr(), keep.data_ptr(),
                                            wt.data_ptr(), dhid.data_ptr(), _p(dhT), _p(dcT), T, B, H,
                                            dgates.data_ptr(), _p(dh0), _p(dc0), stream), "ouz_lstm_seq_bwd")
@@ -373,3 +381,57 @@ class LSTMSequence(torch.autograd.Function):
         dh0 = dgates[0].mm(w_hh) * k0 if ctx.needs_input_grad[1] else None
         dc0 = dc * k0 if ctx.needs_input_grad[2] else None
         return dgates, dh0, dc0, None, d_w
+
+
+class ClipAdam:
+    """``nn.utils.clip_grad_norm_(params, max_norm)`` + ``optimizer.step()`` (RPO-LSTM/agent.py:124-134) as two HIP
+    launches (``ouz_adam_clip_step``) instead of torch's per-tensor norms, their stack / norm / clamp / scale and the
+    multi-tensor Adam kernel.  ``optimizer`` is a plain ``torch.optim.Adam`` (one parameter group, f32 CUDA
+    parameters, no weight decay / amsgrad / maximize): it keeps the parameter group, the hyper-parameters and the
+    state (``step`` on the host, ``exp_avg``, ``exp_avg_sq``), so its ``state_dict`` / ``load_state_dict`` are the
+    reference's checkpoint files unchanged; only its ``step`` is replaced.  The clipped gradients are not written
+    back into ``.grad`` (nothing reads them after the step)."""
+
+    def __init__(self, optimizer):
+        (group,) = optimizer.param_groups
+        if (group["weight_decay"] or group["amsgrad"] or group["maximize"] or len(group["params"]) > L.ADAM_MAX_TENSORS
+                or any(p.dtype != torch.float32 or p.device.type != "cuda" for p in group["params"])):
+            raise ValueError("ClipAdam: one group of <= 16 f32 CUDA tensors, plain Adam")
+        self.optimizer = optimizer
+        self.device = group["params"][0].device
+        self.ws = torch.empty(256, device=self.device)
+
+    def step(self, max_norm):
+        (group,) = self.optimizer.param_groups
+        table = L.OuzAdamTable()
+        keep = []
+        n, step = 0, None
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            st = self.optimizer.state[p]
+            if not st:   # torch's lazy state (Adam._init_group, non-fused form: the step count on the host)
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if st["step"].device.type != "cpu":
+                st["step"] = st["step"].cpu()
+            st["step"] += 1
+            s = int(st["step"])
+            if step is None:
+                step = s
+            elif s != step:
+                raise ValueError("ClipAdam: parameters at different Adam step counts")
+            g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+            keep.append(g)
+            table.numel[n] = p.numel()
+            table.grad[n], table.param[n] = g.data_ptr(), p.data_ptr()
+            table.exp_avg[n], table.exp_avg_sq[n] = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
+            n += 1
+        if n == 0:
+            return
+        table.n_tensors = n
+        b1, b2 = group["betas"]
+        L.check(L.lib.ouz_adam_clip_step(table, float(group["lr"]), float(b1), float(b2), float(group["eps"]), step,
+                                         float(max_norm or 0.0), self.ws.data_ptr(), L.stream_ptr(self.device)),
+                "ouz_adam_clip_step")

@@ -28,7 +28,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import _lib as L
-from .fused import PolicyLoss, ValueLoss
+from .fused import ClipAdam, PolicyLoss, ValueLoss
 from .gemm_tuning import enable_tuned_gemms
 from .models import Critic, LSTMActor, MLPActor
 
@@ -123,8 +123,14 @@ class PPOLearner:
         # fused Adam on the GPU: one multi-tensor kernel per optimizer step instead of the foreach
         # form's handful per parameter group (the update is launch-bound)
         fused = self.device.type == "cuda" and os.environ.get("OUZ_ADAM_FUSED", "1") != "0"
-        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr, eps=1e-5, fused=fused)
-        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=lr, eps=1e-5, fused=fused)
+        # gradient clipping + Adam as two HIP launches per optimizer step (fused.ClipAdam; the torch optimizer keeps
+        # the state and the checkpoint format); OUZ_CLIP_ADAM=0 keeps clip_grad_norm_ + the torch step
+        clip_adam = fused and os.environ.get("OUZ_CLIP_ADAM", "1") != "0"
+        opt_kw = {"foreach": False} if clip_adam else {"fused": fused}
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=lr, eps=1e-5, **opt_kw)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), lr=lr, eps=1e-5, **opt_kw)
+        self._clip_adam = ((ClipAdam(self.actor_optimizer), ClipAdam(self.critic_optimizer)) if clip_adam
+                           else None)
 
     # ------------------------------------------------------------------ rollout
     @torch.no_grad()
@@ -229,19 +235,25 @@ class PPOLearner:
                 self.actor_optimizer.zero_grad()
                 actor_loss.backward()
                 allreduce_grads(self.actor)            # data parallel over ranks (no-op on one GPU)
-                nn.utils.clip_grad_norm_(self.actor.parameters(), self.max_grad_norm)
-                self.actor_optimizer.step()
+                self._clip_step(0, self.actor, self.actor_optimizer)
 
                 self.critic_optimizer.zero_grad()
                 critic_loss.backward()
                 allreduce_grads(self.critic)
-                nn.utils.clip_grad_norm_(self.critic.parameters(), self.max_grad_norm)
-                self.critic_optimizer.step()
+                self._clip_step(1, self.critic, self.critic_optimizer)
                 stats = {"pg_loss": pg_loss.detach(), "v_loss": v_loss.detach(), "approx_kl": approx_kl}
             if self.target_kl is not None and float(stats["approx_kl"]) > self.target_kl:
                 break
         stats["clipfrac"] = clipfracs / max(n_mb, 1)
         return stats
+
+    def _clip_step(self, which, net, optimizer):
+        """clip_grad_norm_(net, max_grad_norm) + optimizer.step() (agent.py:124-134)."""
+        if self._clip_adam is not None:
+            self._clip_adam[which].step(self.max_grad_norm)
+        else:
+            nn.utils.clip_grad_norm_(net.parameters(), self.max_grad_norm)
+            optimizer.step()
 
     # -------------------------------------------------------------- checkpoints
     def save(self, filename):

@@ -432,3 +432,51 @@ def test_policy_sample_kernel_matches_the_direct_form(B, H):
     torch.testing.assert_close(got[0], want[0], rtol=1e-5, atol=2e-6)
     torch.testing.assert_close(got[1], want[1], rtol=1e-5, atol=2e-6)
     torch.testing.assert_close(got[2], want[2].contiguous(), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 0.0])
+def test_clip_adam_matches_torch_clip_and_adam(max_norm):
+    """fused.ClipAdam (ouz_adam_clip_step: clip_grad_norm_ + Adam.step in two launches) against
+    nn.utils.clip_grad_norm_ + torch.optim.Adam over 6 steps of the actor's parameters, with the clip active on the
+    large-gradient steps and inactive on the small ones (and off: max_norm 0); then its state dict loads into a
+    plain torch Adam with the same step counts."""
+    from ouzelum_amd.learners.fused import ClipAdam
+    from ouzelum_amd.learners.models import LSTMActor
+    from ouzelum_amd.spaces import Box
+    obs_s, act_s = Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))
+    torch.manual_seed(5)
+    ref = LSTMActor(obs_s, act_s).cuda()
+    new = LSTMActor(obs_s, act_s).cuda()
+    new.load_state_dict(ref.state_dict())
+    opt_ref = torch.optim.Adam(ref.parameters(), lr=2.6e-3, eps=1e-5, foreach=False)
+    opt_new = torch.optim.Adam(new.parameters(), lr=2.6e-3, eps=1e-5, foreach=False)
+    ca = ClipAdam(opt_new)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for step in range(6):
+        scale = 1.0 if step % 2 == 0 else 1e-3   # total norm >> 1 (clipped) / << 1 (not clipped)
+        for pr, pn in zip(ref.parameters(), new.parameters()):
+            gr = torch.randn(pr.shape, device="cuda", generator=g) * scale
+            pr.grad, pn.grad = gr.clone(), gr.clone()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm)
+        opt_ref.step()
+        ca.step(max_norm)
+    for (name, pr), pn in zip(ref.named_parameters(), new.parameters()):
+        sr, sn = opt_ref.state[pr], opt_new.state[pn]
+        assert float(sr["step"]) == float(sn["step"]) == 6.0
+        for key in ("exp_avg", "exp_avg_sq"):
+            err = float((sr[key] - sn[key]).abs().max() / sr[key].abs().max().clamp_min(1e-12))
+            assert err < 2e-5, (name, key, err)
+        assert float((pr - pn).abs().max()) < 2e-6, name
+    loaded = torch.optim.Adam(ref.parameters(), lr=2.6e-3, eps=1e-5)
+    loaded.load_state_dict(opt_new.state_dict())
+    assert all(float(s["step"]) == 6.0 for s in loaded.state.values())
+
+
+def test_clip_adam_refuses_what_it_does_not_compute():
+    from ouzelum_amd.learners.fused import ClipAdam
+    lin = torch.nn.Linear(4, 4).cuda()
+    with pytest.raises(ValueError):
+        ClipAdam(torch.optim.Adam(lin.parameters(), weight_decay=0.1))
+    with pytest.raises(ValueError):
+        ClipAdam(torch.optim.Adam([torch.nn.Parameter(torch.zeros(2, device="cuda")) for _ in range(17)]))
