@@ -174,3 +174,18 @@ def test_tensorboard_event_file_round_trips(tmp_path):
     with pytest.raises(ValueError, match="CRC"):
         TB.read_records(str(bad))
     assert struct.calcsize("<Q") == 8
+
+
+def test_clip_adam_refuses_cpu_and_unsupported_optimizers():
+    """fused.ClipAdam (the two-launch clip + Adam step) takes plain Adam over f32 CUDA tensors only; anything else is
+    refused at construction, and PPOLearner on the CPU keeps torch's clip_grad_norm_ + Adam."""
+    import torch
+    from ouzelum_amd.learners.fused import ClipAdam
+    lin = torch.nn.Linear(4, 4)
+    with pytest.raises(ValueError):
+        ClipAdam(torch.optim.Adam(lin.parameters()))
+    from ouzelum_amd.learners import PPOLearner
+    from ouzelum_amd.spaces import Box
+    obs_s, act_s = Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))
+    ag = PPOLearner(obs_s, act_s, 8, "cpu", recurrent=False, num_minibatches=1, update_epochs=1)
+    assert ag._clip_adam is None
