@@ -90,6 +90,38 @@ def test_learner_loss_entry_points_validate_without_gpu(L):
     assert b"null buffer" in L.lib.ouz_last_error()
 
 
+def test_lstm_seq_and_adam_entry_points_validate_without_gpu(L):
+    """The sequence-kernel and clipped-Adam entry points refuse bad sizes, misaligned or inconsistent buffers and bad
+    tables before launching anything (fake device addresses: nothing is dereferenced on the host)."""
+    A, M = 0x10000, 0x10004   # a 16-byte aligned and a misaligned fake address
+    fwd = L.lib.ouz_lstm_seq_fwd
+    assert fwd(A, A, A, A, A, 16, 8, 64, None, None, A, None, None, None, None, None) == -1
+    assert b"H must be 128" in L.lib.ouz_last_error()
+    assert fwd(M, A, A, A, A, 16, 8, 128, None, None, A, None, None, None, None, None) == -1
+    assert b"16-byte aligned" in L.lib.ouz_last_error()
+    assert fwd(A, A, A, A, A, 16, 8, 128, A, None, A, A, A, None, None, None) == -1
+    assert b"all four or none" in L.lib.ouz_last_error()
+    assert fwd(A, A, A, A, A, 16, 8, 128, None, None, A, None, None, A, None, None) == -1   # h_out without c_out
+    bwd = L.lib.ouz_lstm_seq_bwd
+    assert bwd(A, A, A, A, A, A, None, None, 16, 8, 128, M, None, None, None) == -1
+    assert b"16-byte aligned" in L.lib.ouz_last_error()
+    assert bwd(A, A, A, A, A, A, None, None, 0, 8, 128, A, None, None, None) == -1
+    assert ctypes.sizeof(L.OuzAdamTable) == 8 + 5 * 8 * L.ADAM_MAX_TENSORS
+    t = L.OuzAdamTable()
+    ws = A
+    for n in (0, L.ADAM_MAX_TENSORS + 1):
+        t.n_tensors = n
+        assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 1, 1.0, ws, None) == -1
+        assert b"tensors" in L.lib.ouz_last_error()
+    t.n_tensors, t.numel[0] = 1, 4
+    t.grad[0] = t.param[0] = t.exp_avg[0] = A
+    assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 1, 1.0, ws, None) == -1      # exp_avg_sq null
+    assert b"null tensor" in L.lib.ouz_last_error()
+    t.exp_avg_sq[0] = A
+    assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 0, 1.0, ws, None) == -1      # steps count from 1
+    assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 1, 1.0, None, None) == -1    # no workspace
+
+
 def test_struct_layout(L):
     # must equal the static_asserts in quad_kernels.hip
     assert ctypes.sizeof(L.OuzConfig) == 88
