@@ -68,7 +68,7 @@ extern "C" {
                                   ouz_policy_sample);
                                6: sim_params gravity domain randomisation (ouz_set_dr_gravity), the fused LSTM
                                   sequence kernels (ouz_lstm_seq_fwd / ouz_lstm_seq_bwd), clipped Adam
-                                  (ouz_adam_clip_step) */
+                                  (ouz_adam_clip_step), the small-K first layer (ouz_linear_tanh_small_k) */
 
 /* error codes */
 #define OUZ_OK 0
@@ -439,12 +439,19 @@ int ouz_lstm_seq_bwd(const float* act, const float* c_all, const float* cm, cons
                      const float* dhid, const float* dhT, const float* dcT, int32_t T, int32_t B, int32_t H,
                      float* dgates, float* dh0, float* dc0, void* stream);
 
+/* The trunks' first layer in one pass: y [rows][cols] = tanh(x [rows][K] W^T + b), W [cols][K] (nn.Linear's
+ * weight), 1 <= K <= 16 (the 13 observations: RPO-LSTM/model.py:11-20 and the critic), cols a power of two in
+ * [4, 1024], y 16-byte aligned.  tanh to ~1e-7 absolute (hardware exp2 / reciprocal). */
+int ouz_linear_tanh_small_k(const float* x, const float* w, const float* b, int32_t rows, int32_t K, int32_t cols,
+                            float* y, void* stream);
+
 /* Gradient-norm clipping + Adam over one network's parameter tensors in two launches (RPO-LSTM/agent.py:124-134:
  * nn.utils.clip_grad_norm_(params, max_norm) then torch.optim.Adam.step(); torch/optim/adam.py single-tensor order).
  * The table lists up to OUZ_ADAM_MAX_TENSORS f32 tensors (contiguous, numel elements each): gradient (read only),
  * parameter, exp_avg and exp_avg_sq (updated in place).  step: the Adam step count after this step (1, 2, ...);
- * max_norm <= 0: no clipping.  workspace: 256 floats of device memory. */
+ * max_norm <= 0: no clipping.  workspace: OUZ_ADAM_WS_FLOATS floats of device memory. */
 #define OUZ_ADAM_MAX_TENSORS 16
+#define OUZ_ADAM_WS_FLOATS 512
 typedef struct ouz_adam_table {
   int32_t n_tensors;
   int32_t reserved;

@@ -92,6 +92,7 @@ class OuzTaskInfo(ctypes.Structure):
 
 
 ADAM_MAX_TENSORS = 16   # OUZ_ADAM_MAX_TENSORS
+ADAM_WS_FLOATS = 512    # OUZ_ADAM_WS_FLOATS
 
 
 class OuzAdamTable(ctypes.Structure):
@@ -160,6 +161,7 @@ SIGNATURES = {
     "ouz_ppo_value_loss": (_I, [_P, _P, _I, _P, _P, _P, _P]),
     "ouz_tanh_bwd_bias": (_I, [_P, _P, _I, _I, _P, _P, _P, _P]),
     "ouz_policy_sample": (_I, [_P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P]),
+    "ouz_linear_tanh_small_k": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "ouz_adam_clip_step": (_I, [ctypes.POINTER(OuzAdamTable), ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_double, _I64, ctypes.c_double, _P, _P]),
 }

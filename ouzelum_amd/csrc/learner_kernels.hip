@@ -10,6 +10,7 @@
 //    of a CPU torch.rand coin + a CPU noise tensor copied H2D every step.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <string>
@@ -774,13 +775,16 @@ int launch_status(const char* what) {
 // nn.utils.clip_grad_norm_(parameters, max_grad_norm) then optim.Adam.step()), in place of torch's per-tensor norms,
 // their stack / norm / clamp / scale launches and the multi-tensor Adam kernel (~6 launches and ~70 us per step on a
 // < 1 M-parameter network: the multi-tensor kernel's grid is sized by tensor chunks, not by the chip).
-//   adam_sqnorm_kernel: kAdamBlocks partial sums of g^2 over every tensor of the table (grid-stride, fixed order);
+//   the parameters are cut into chunks of ch elements, one block per chunk (a uniform scan finds the block's tensor),
+//   ch = max(1024, the total / 256 rounded up to 1024), so at most 256 + 16 blocks; each thread loads its (up to) four
+//   elements of a pass before it uses them, one memory round trip per pass;
+//   adam_sqnorm_kernel: one partial sum of g^2 per chunk (fixed order);
 //   adam_step_kernel: every block reduces the same partials in the same order (so all agree on the norm without a
 //   third launch), clip coefficient min(max_norm / (||g|| + 1e-6), 1) as torch computes it, then the Adam update in
 //   torch's single-tensor order (exp_avg.lerp_, exp_avg_sq.mul_.addcmul_, denom = sqrt(v) / sqrt(bc2) + eps,
 //   param.addcdiv_(m, denom, -lr / bc1)).  The clipped gradient is not written back (nothing reads it after step).
 // ---------------------------------------------------------------------------
-constexpr int kAdamBlocks = 256;
+constexpr int kAdamMinChunk = 1024;
 
 __device__ __forceinline__ float block_sum256(float v, float* red) {
   red[threadIdx.x] = v;
@@ -795,40 +799,115 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return r;
 }
 
-__global__ void __launch_bounds__(256) adam_sqnorm_kernel(ouz_adam_table t, float* __restrict__ part) {
+// The block's tensor and element range [lo, hi) (uniform across the block).
+__device__ __forceinline__ int adam_chunk(const ouz_adam_table& t, int64_t ch, int64_t& lo, int64_t& hi) {
+  int64_t cb = blockIdx.x;
+  int i = 0;
+  for (; i < t.n_tensors; ++i) {
+    const int64_t n = (t.numel[i] + ch - 1) / ch;
+    if (cb < n) break;
+    cb -= n;
+  }
+  lo = cb * ch;
+  hi = lo + ch < t.numel[i] ? lo + ch : t.numel[i];
+  return i;
+}
+
+__global__ void __launch_bounds__(256) adam_sqnorm_kernel(ouz_adam_table t, int64_t ch, float* __restrict__ part) {
   __shared__ float red[256];
-  const int64_t stride = (int64_t)gridDim.x * 256, g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int64_t lo, hi;
+  const int i = adam_chunk(t, ch, lo, hi);
+  const float* __restrict__ g = t.grad[i];
   float acc = 0.0f;
-  for (int i = 0; i < t.n_tensors; ++i) {
-    const float* g = t.grad[i];
-    for (int64_t e = g0; e < t.numel[i]; e += stride) acc += g[e] * g[e];
+  for (int64_t e0 = lo + threadIdx.x; e0 < hi; e0 += 4 * 256) {
+    float gv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gv[u] = e0 + 256 * u < hi ? g[e0 + 256 * u] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += gv[u] * gv[u];
   }
   const float s = block_sum256(acc, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
-__global__ void __launch_bounds__(256) adam_step_kernel(ouz_adam_table t, const float* __restrict__ part, float lr_bc1,
-                                                        float w1, float beta2, float w2, float eps, float bc2_sqrt,
-                                                        float max_norm) {
+__global__ void __launch_bounds__(256) adam_step_kernel(ouz_adam_table t, int64_t ch, const float* __restrict__ part,
+                                                        int nparts, float lr_bc1, float w1, float beta2, float w2,
+                                                        float eps, float bc2_sqrt, float max_norm) {
   __shared__ float red[256];
   float coef = 1.0f;
   if (max_norm > 0.0f) {
-    const float total = sqrtf(block_sum256(part[threadIdx.x], red));
+    float v = 0.0f;
+    for (int j = threadIdx.x; j < nparts; j += 256) v += part[j];
+    const float total = sqrtf(block_sum256(v, red));
     coef = fminf(max_norm / (total + 1e-6f), 1.0f);
   }
-  const int64_t stride = (int64_t)gridDim.x * 256, g0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  for (int i = 0; i < t.n_tensors; ++i) {
-    const float* g = t.grad[i];
-    float* p = t.param[i];
-    float* m = t.exp_avg[i];
-    float* v = t.exp_avg_sq[i];
-    for (int64_t e = g0; e < t.numel[i]; e += stride) {
-      const float gc = g[e] * coef;
-      const float mn = m[e] + w1 * (gc - m[e]);   // lerp(m, g, 1 - beta1)
-      const float vn = v[e] * beta2 + w2 * gc * gc;
+  int64_t lo, hi;
+  const int i = adam_chunk(t, ch, lo, hi);
+  const float* __restrict__ g = t.grad[i];
+  float* __restrict__ p = t.param[i];
+  float* __restrict__ m = t.exp_avg[i];
+  float* __restrict__ v = t.exp_avg_sq[i];
+  for (int64_t e0 = lo + threadIdx.x; e0 < hi; e0 += 4 * 256) {
+    float gv[4], mv[4], vv[4], pv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = e0 + 256 * u;
+      if (e < hi) { gv[u] = g[e]; mv[u] = m[e]; vv[u] = v[e]; pv[u] = p[e]; }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = e0 + 256 * u;
+      if (e >= hi) continue;
+      const float gc = gv[u] * coef;
+      const float mn = mv[u] + w1 * (gc - mv[u]);   // lerp(m, g, 1 - beta1)
+      const float vn = vv[u] * beta2 + w2 * gc * gc;
       m[e] = mn;
       v[e] = vn;
-      p[e] = p[e] + (-lr_bc1) * (mn / (sqrtf(vn) / bc2_sqrt + eps));
+      p[e] = pv[u] + (-lr_bc1) * (mn / (sqrtf(vn) / bc2_sqrt + eps));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// The trunks' first layer, y = tanh(x W^T + b) with K <= 16 inputs (the 13 observations; RPO-LSTM/model.py:11-20,
+// agent.py critic), in ONE pass: hipBLASLt's K = 13 GEMM writes the pre-activation and torch's tanh reads and rewrites
+// it, where this layer is a write of y and nothing else.  W^T, b and a chunk of rows' inputs sit in LDS; each thread
+// makes four consecutive outputs of a row (one 16-byte store).  tanh is the sequence kernels' ftanh.
+// (A round-5 form with one thread per row and a column loop waited on its rows' loads one after another and lost to
+// the GEMM + tanh pair at 65 536 rows; docs/HISTORY.md.)
+// ---------------------------------------------------------------------------
+constexpr int kSmallKMax = 16;
+constexpr int kSmallKBlocks = 1024;
+constexpr int kSmallKChunk = 64;   // at most this many rows' inputs staged in LDS at a time (fewer below 32 K rows)
+
+__global__ void __launch_bounds__(256) linear_tanh_smallk_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                                 const float* __restrict__ b, int rows, int K, int cols,
+                                                                 int chunk, float* __restrict__ y) {
+  extern __shared__ float sw[];   // W^T [K][cols], b [cols], then the chunk's inputs [chunk][K]
+  float* sx = sw + (K + 1) * cols;
+  for (int e = threadIdx.x; e < K * cols; e += 256) {
+    const int k = e / cols, c = e - k * cols;
+    sw[e] = w[(size_t)c * K + k];
+  }
+  for (int c = threadIdx.x; c < cols; c += 256) sw[K * cols + c] = b[c];
+  const int tpr = cols >> 2, rpb = 256 / tpr;   // threads per row, rows per pass (cols a power of two)
+  const int c4 = (int)threadIdx.x % tpr, rs = (int)threadIdx.x / tpr;
+  // the block's rows: contiguous chunks, dealt round robin over the blocks; each chunk's inputs are one coalesced
+  // load into LDS, so no thread waits on its rows' input loads one after another
+  for (int r0 = blockIdx.x * chunk; r0 < rows; r0 += gridDim.x * chunk) {
+    const int nr = rows - r0 < chunk ? rows - r0 : chunk;
+    __syncthreads();   // W^T / b written (first chunk), every thread done with the previous chunk's inputs
+    for (int e = threadIdx.x; e < nr * K; e += 256) sx[e] = x[(size_t)r0 * K + e];
+    __syncthreads();
+    const f32x4 bias = ld4(&sw[K * cols + 4 * c4]);
+    for (int r = rs; r < nr; r += rpb) {
+      f32x4 acc = bias;
+#pragma unroll 4
+      for (int k = 0; k < K; ++k) acc += sx[r * K + k] * ld4(&sw[k * cols + 4 * c4]);
+      f32x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = ftanh(acc[i]);
+      st4(y + (size_t)(r0 + r) * cols + 4 * c4, o);
     }
   }
 }
@@ -1035,12 +1114,37 @@ int ouz_adam_clip_step(const ouz_adam_table* t, double lr, double beta1, double 
       return set_error(OUZ_ERR_INVALID, "ouz_adam_clip_step: null tensor in the table");
   // torch's host-side scalars (Adam's non-capturable path): computed in double (Python floats), used as f32
   const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+  int64_t total = 0;
+  for (int i = 0; i < t->n_tensors; ++i) total += t->numel[i];
+  if (total == 0) return OUZ_OK;
+  const int64_t ch = std::max<int64_t>(kAdamMinChunk, (total / 256 + kAdamMinChunk) / kAdamMinChunk * kAdamMinChunk);
+  int64_t chunks = 0;
+  for (int i = 0; i < t->n_tensors; ++i) chunks += (t->numel[i] + ch - 1) / ch;
+  // (chunks <= 256 + OUZ_ADAM_MAX_TENSORS <= OUZ_ADAM_WS_FLOATS; a zero-element tensor owns no chunk and no block)
   const hipStream_t s = (hipStream_t)stream;
-  if (max_norm > 0.0) hipLaunchKernelGGL(adam_sqnorm_kernel, dim3(kAdamBlocks), dim3(256), 0, s, *t, workspace);
-  hipLaunchKernelGGL(adam_step_kernel, dim3(kAdamBlocks), dim3(256), 0, s, *t, workspace, (float)(lr / bc1),
-                     (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps, (float)std::sqrt(bc2),
-                     (float)max_norm);
+  if (max_norm > 0.0)
+    hipLaunchKernelGGL(adam_sqnorm_kernel, dim3((unsigned)chunks), dim3(256), 0, s, *t, ch, workspace);
+  hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)chunks), dim3(256), 0, s, *t, ch, workspace, (int)chunks,
+                     (float)(lr / bc1), (float)(1.0 - beta1), (float)beta2, (float)(1.0 - beta2), (float)eps,
+                     (float)std::sqrt(bc2), (float)max_norm);
   return launch_status("adam_step_kernel");
+}
+
+
+int ouz_linear_tanh_small_k(const float* x, const float* w, const float* b, int32_t rows, int32_t K, int32_t cols,
+                            float* y, void* stream) {
+  if (rows < 0 || K < 1 || K > kSmallKMax || cols < 4 || cols > 1024 || (cols & (cols - 1)))
+    return set_error(OUZ_ERR_INVALID, "ouz_linear_tanh_small_k: rows >= 0, 1 <= K <= 16, cols a power of two in [4, 1024]");
+  if (rows == 0) return OUZ_OK;   // (torch's empty tensors have null data pointers)
+  if (!x || !w || !b || !y) return set_error(OUZ_ERR_INVALID, "ouz_linear_tanh_small_k: null buffer");
+  if (!aligned16(y)) return set_error(OUZ_ERR_INVALID, "ouz_linear_tanh_small_k: y must be 16-byte aligned");
+  // chunks of 8-64 rows: at least ~512 blocks where the rows allow (the rollout's 8 192 rows: 16-row chunks)
+  const int chunk = std::max(8, std::min(kSmallKChunk, (rows + 511) / 512));
+  const int blocks = std::min((rows + chunk - 1) / chunk, kSmallKBlocks);
+  hipLaunchKernelGGL(linear_tanh_smallk_kernel, dim3(blocks), dim3(256),
+                     ((size_t)(K + 1) * cols + (size_t)chunk * K) * sizeof(float), (hipStream_t)stream, x, w, b, rows, K,
+                     cols, chunk, y);
+  return launch_status("linear_tanh_smallk_kernel");
 }
 
 }  // extern "C"

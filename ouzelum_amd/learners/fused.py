@@ -30,6 +30,9 @@ _SEQ = os.environ.get("OUZ_LSTM_SEQ", "1") != "0"
 SEQ_H = 128
 _FUSED_TANH = os.environ.get("OUZ_FUSED_TANH", "1") != "0"
 _FUSED_SAMPLE = os.environ.get("OUZ_FUSED_SAMPLE", "1") != "0"
+# the trunks' first layer (K <= 16 inputs) + tanh in one HIP pass (ouz_linear_tanh_small_k); OUZ_SMALLK_TANH=0 keeps
+# hipBLASLt's GEMM + torch's tanh
+_SMALLK_TANH = os.environ.get("OUZ_SMALLK_TANH", "1") != "0"
 
 
 def _splits(k, n_out_tiles):
@@ -69,14 +72,34 @@ class SplitKLinear(torch.autograd.Function):
         return dx, dw, db
 
 
+def smallk_ok(x, weight, bias):
+    """``linear_tanh_small_k`` applies: f32 CUDA rows, K <= 16 inputs, a power-of-two width in [4, 1024], a bias."""
+    cols, k = weight.shape
+    return (_SMALLK_TANH and bias is not None and x.is_cuda and x.dtype == torch.float32 and x.dim() == 2
+            and 1 <= k <= 16 and 4 <= cols <= 1024 and cols & (cols - 1) == 0)
+
+
+def linear_tanh_small_k(x, weight, bias):
+    """tanh(x Wᵀ + b) for a first layer of K <= 16 inputs in one pass (``ouz_linear_tanh_small_k``; no autograd)."""
+    x = x.contiguous()
+    w, b = weight.detach().contiguous(), bias.detach().contiguous()
+    y = torch.empty((x.shape[0], w.shape[0]), device=x.device)
+    L.check(L.lib.ouz_linear_tanh_small_k(x.data_ptr(), w.data_ptr(), b.data_ptr(), x.shape[0], w.shape[1], w.shape[0],
+                                          y.data_ptr(), L.stream_ptr(x.device)), "ouz_linear_tanh_small_k")
+    return y
+
+
 class LinearTanh(torch.autograd.Function):
-    """y = tanh(x Wᵀ + b); backward: dz = dy (1 - y²) and db = Σ_rows dz in one HIP pass, then dx = dz W and the
-    split-K dW = dzᵀ x."""
+    """y = tanh(x Wᵀ + b) (one HIP pass where K <= 16: ``linear_tanh_small_k``); backward: dz = dy (1 - y²) and
+    db = Σ_rows dz in one HIP pass, then dx = dz W and the split-K dW = dzᵀ x."""
 
     @staticmethod
     def forward(ctx, x, weight, bias):
-        y = torch.addmm(bias, x, weight.t())
-        torch.tanh_(y)
+        if smallk_ok(x, weight, bias):
+            y = linear_tanh_small_k(x, weight, bias)
+        else:
+            y = torch.addmm(bias, x, weight.t())
+            torch.tanh_(y)
         ctx.save_for_backward(x, weight, y)
         return y
 
@@ -114,16 +137,21 @@ def _tanh_fusable(layer, x, min_rows):
 
 def run_mlp(seq, x, min_rows=8192):
     """Forward through an nn.Sequential of Linear / activation modules using ``linear``; a Linear followed by a
-    Tanh becomes one ``LinearTanh`` where its rows and width allow."""
+    Tanh becomes one ``LinearTanh`` where its rows and width allow, and, without autograd (the rollout's policy and
+    value calls), a first layer of K <= 16 inputs + its Tanh one ``linear_tanh_small_k`` pass at any row count."""
     mods = list(seq)
     i = 0
     while i < len(mods):
         m = mods[i]
-        if (isinstance(m, torch.nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.Tanh)
-                and _tanh_fusable(m, x, min_rows)):
-            x = LinearTanh.apply(x, m.weight, m.bias)
-            i += 2
-            continue
+        if isinstance(m, torch.nn.Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], torch.nn.Tanh):
+            if _tanh_fusable(m, x, min_rows):
+                x = LinearTanh.apply(x, m.weight, m.bias)
+                i += 2
+                continue
+            if not torch.is_grad_enabled() and smallk_ok(x, m.weight, m.bias):
+                x = linear_tanh_small_k(x, m.weight, m.bias)
+                i += 2
+                continue
         x = linear(x, m, min_rows) if isinstance(m, torch.nn.Linear) else m(x)
         i += 1
     return x
@@ -399,7 +427,7 @@ class ClipAdam:
             raise ValueError("ClipAdam: one group of <= 16 f32 CUDA tensors, plain Adam")
         self.optimizer = optimizer
         self.device = group["params"][0].device
-        self.ws = torch.empty(256, device=self.device)
+        self.ws = torch.empty(L.ADAM_WS_FLOATS, device=self.device)
 
     def step(self, max_norm):
         (group,) = self.optimizer.param_groups

@@ -31,6 +31,10 @@ def category(name):
     if any(k in name for k in ("policy_loss_kernel", "value_loss_kernel", "loss_finish_kernel", "adv_moments_kernel",
                                 "tanh_bwd_colsum_kernel", "colsum_finish_kernel")):
         return "PPO losses + trunk tanh'/bias (HIP)"
+    if "linear_tanh_smallk" in name:
+        return "trunks' first layer + tanh (HIP, one pass)"
+    if "adam_step_kernel" in name or "adam_sqnorm_kernel" in name:
+        return "clipped Adam (HIP, two launches)"
     if "FusedOptimizer" in name or "multi_tensor_apply" in name:
         return "fused Adam / grad-norm (multi-tensor)"
     if "reduce_kernel" in name:

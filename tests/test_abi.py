@@ -120,6 +120,12 @@ def test_lstm_seq_and_adam_entry_points_validate_without_gpu(L):
     t.exp_avg_sq[0] = A
     assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 0, 1.0, ws, None) == -1      # steps count from 1
     assert L.lib.ouz_adam_clip_step(t, 1e-3, 0.9, 0.999, 1e-5, 1, 1.0, None, None) == -1    # no workspace
+    st = L.lib.ouz_linear_tanh_small_k
+    assert st(A, A, A, 16, 17, 512, A, None) == -1 and b"K <= 16" in L.lib.ouz_last_error()
+    assert st(A, A, A, 16, 13, 384, A, None) == -1 and b"power of two" in L.lib.ouz_last_error()
+    assert st(A, A, A, 16, 13, 512, M, None) == -1 and b"16-byte aligned" in L.lib.ouz_last_error()
+    assert st(A, None, A, 16, 13, 512, A, None) == -1 and b"null buffer" in L.lib.ouz_last_error()
+    assert st(A, A, A, 0, 13, 512, A, None) == 0   # no rows: nothing to launch
 
 
 def test_struct_layout(L):

@@ -480,3 +480,23 @@ def test_clip_adam_refuses_what_it_does_not_compute():
         ClipAdam(torch.optim.Adam(lin.parameters(), weight_decay=0.1))
     with pytest.raises(ValueError):
         ClipAdam(torch.optim.Adam([torch.nn.Parameter(torch.zeros(2, device="cuda")) for _ in range(17)]))
+
+
+@pytest.mark.parametrize("rows,k,cols", [(65536, 13, 512), (8195, 13, 256), (3, 1, 4), (1000, 16, 1024), (0, 13, 512)])
+def test_linear_tanh_small_k_matches_torch(rows, k, cols):
+    """ouz_linear_tanh_small_k (first layer + tanh in one pass) against torch.tanh(F.linear) in f32, and run_mlp's
+    no-autograd path (the rollout's policy / value calls) against the torch modules."""
+    from ouzelum_amd.learners.fused import linear_tanh_small_k, run_mlp
+    torch.manual_seed(rows + k + cols)
+    lin = torch.nn.Linear(k, cols).cuda()
+    x = torch.randn(rows, k, device="cuda")
+    with torch.no_grad():
+        ref = torch.tanh(lin(x))
+        y = linear_tanh_small_k(x, lin.weight, lin.bias)
+        assert y.shape == ref.shape
+        if rows:
+            assert float((y - ref).abs().max()) < 5e-6
+        seq = torch.nn.Sequential(lin, torch.nn.Tanh(), torch.nn.Linear(cols, 8).cuda())
+        out, want = run_mlp(seq, x), seq(x)
+        if rows:
+            assert float((out - want).abs().max() / want.abs().max().clamp_min(1e-6)) < 2e-5
