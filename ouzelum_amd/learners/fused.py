@@ -463,3 +463,18 @@ class ClipAdam:
         L.check(L.lib.ouz_adam_clip_step(table, float(group["lr"]), float(b1), float(b2), float(group["eps"]), step,
                                          float(max_norm or 0.0), self.ws.data_ptr(), L.stream_ptr(self.device)),
                 "ouz_adam_clip_step")
+
+
+_FOREACH_COPY = os.environ.get("OUZ_FOREACH_COPY", "1") != "0"
+
+
+def store(dsts, srcs):
+    """dst.copy_(src) for each pair, as ONE multi-tensor launch (torch._foreach_copy_) where all are CUDA tensors of
+    one dtype: the rollout loop's per-step storage writes (5 copies per step: 20 against 8.6 µs,
+    ``scripts/exp/copy_gather_probe.py``); ``OUZ_FOREACH_COPY=0`` keeps one copy each."""
+    if (_FOREACH_COPY and all(t.is_cuda for t in (*dsts, *srcs))
+            and len({t.dtype for t in (*dsts, *srcs)}) == 1):
+        torch._foreach_copy_(list(dsts), list(srcs))
+    else:
+        for d, s in zip(dsts, srcs):
+            d.copy_(s)

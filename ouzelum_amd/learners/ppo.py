@@ -179,6 +179,11 @@ class PPOLearner:
         b_advantages = advantages.reshape(-1)
         b_returns = returns.reshape(-1)
         flatinds = torch.arange(T * N, device=self.device).reshape(T, N)
+        # the minibatch's four per-row scalars as ONE gather of their stacked rows (each result row contiguous)
+        # instead of four (OUZ_STACKED_GATHER=0: one per tensor); exact either way
+        scalars = [b_logprobs, b_dones, b_advantages, b_returns]
+        stacked = (torch.stack([x.float() for x in scalars]) if self.device.type == "cuda"
+                   and os.environ.get("OUZ_STACKED_GATHER", "1") != "0" else None)
         clipfracs = torch.zeros((), device=self.device)
         n_mb = 0
         # the HIP loss kernels where they compute exactly the loss asked for: no entropy bonus (ent_coef 0, as both
@@ -198,37 +203,43 @@ class PPOLearner:
             for mb_inds, mbenvinds in batches:
                 mb_state = ((initial_lstm_state[0][:, mbenvinds], initial_lstm_state[1][:, mbenvinds])
                             if self.recurrent else None)
+                if stacked is not None:
+                    mb_logp, mb_done, mb_advs, mb_ret = torch.index_select(stacked, 1, mb_inds).unbind(0)
+                else:
+                    mb_logp, mb_done, mb_advs, mb_ret = (x[mb_inds] for x in scalars)
+                mb_pomdps, mb_obs = b_pomdps.index_select(0, mb_inds), b_obs.index_select(0, mb_inds)
+                mb_actions = b_actions.index_select(0, mb_inds)
                 if fused_loss:
                     # the HIP losses (fused.PolicyLoss / ValueLoss): same quantities, ~5 launches instead of ~60
-                    mean_z = (self.actor.update_mean(b_pomdps[mb_inds], mb_state, b_dones[mb_inds]) if self.recurrent
-                              else self.actor.update_mean(b_pomdps[mb_inds]))
+                    mean_z = (self.actor.update_mean(mb_pomdps, mb_state, mb_done) if self.recurrent
+                              else self.actor.update_mean(mb_pomdps))
                     pg_loss, approx_kl, clipfrac = PolicyLoss.apply(
-                        mean_z, self.actor.actor_logstd, b_actions[mb_inds], b_logprobs[mb_inds],
-                        b_advantages[mb_inds], self.clip_coef, self.norm_adv)
-                    newvalue = self.critic(b_obs[mb_inds]).view(-1)
-                    v_loss = ValueLoss.apply(newvalue, b_returns[mb_inds])
+                        mean_z, self.actor.actor_logstd, mb_actions, mb_logp,
+                        mb_advs, self.clip_coef, self.norm_adv)
+                    newvalue = self.critic(mb_obs).view(-1)
+                    v_loss = ValueLoss.apply(newvalue, mb_ret)
                     clipfracs += clipfrac
                     n_mb += 1
                     actor_loss = pg_loss
                 else:
                     if self.recurrent:
-                        _, newlogprob, entropy, _ = self.actor(b_pomdps[mb_inds], mb_state, b_dones[mb_inds],
-                                                               b_actions[mb_inds])
+                        _, newlogprob, entropy, _ = self.actor(mb_pomdps, mb_state, mb_done,
+                                                               mb_actions)
                     else:
-                        _, newlogprob, entropy = self.actor(b_pomdps[mb_inds], b_actions[mb_inds])
-                    newvalue = self.critic(b_obs[mb_inds]).view(-1)
-                    logratio = newlogprob - b_logprobs[mb_inds]
+                        _, newlogprob, entropy = self.actor(mb_pomdps, mb_actions)
+                    newvalue = self.critic(mb_obs).view(-1)
+                    logratio = newlogprob - mb_logp
                     ratio = logratio.exp()
                     with torch.no_grad():
                         approx_kl = ((ratio - 1) - logratio).mean()
                         clipfracs += ((ratio - 1.0).abs() > self.clip_coef).float().mean()
                         n_mb += 1
-                    mb_adv = b_advantages[mb_inds]
+                    mb_adv = mb_advs
                     if self.norm_adv:
                         mb_adv = (mb_adv - mb_adv.mean()) / (mb_adv.std() + 1e-8)
                     pg_loss = torch.max(-mb_adv * ratio,
                                         -mb_adv * torch.clamp(ratio, 1 - self.clip_coef, 1 + self.clip_coef)).mean()
-                    v_loss = 0.5 * ((newvalue - b_returns[mb_inds]) ** 2).mean()
+                    v_loss = 0.5 * ((newvalue - mb_ret) ** 2).mean()
                     actor_loss = pg_loss - self.ent_coef * entropy.mean()
                 critic_loss = v_loss * self.vf_coef
 

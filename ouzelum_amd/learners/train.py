@@ -25,6 +25,7 @@ import torch.distributed as dist
 
 from ..distributed import init_from_env, shard
 from ..vec_task import make
+from .fused import store
 from .ppo import PPOLearner
 from .tbevents import EventWriter
 from .wrappers import ExtractObsWrapper, POMDPWrapper, RecordEpisodeStatisticsTorch
@@ -97,13 +98,10 @@ def train(args):
         init_state = (lstm_state[0].clone(), lstm_state[1].clone()) if lstm_state is not None else None
         for step in range(T):
             global_step += N * world
-            pomdps[step] = pomdp
-            obs[step] = next_obs
-            dones[step] = next_done
+            store((pomdps[step], obs[step], dones[step]), (pomdp, next_obs, next_done))
             act_in = pomdp if args.rollout_obs == "pomdp" else next_obs
             action, logprob, _, lstm_state = agent.act(act_in, lstm_state, next_done, alias=True)
-            actions[step] = action
-            logprobs[step] = logprob
+            store((actions[step], logprobs[step]), (action, logprob))
             next_obs, rewards[step], next_done, info = envs.step(action)
             pomdp = pomdp_w.observation(next_obs)
         stats = agent.train(obs, pomdps, actions, next_obs, next_done, init_state, logprobs, rewards, dones)

@@ -14,6 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ouzelum_amd.learners import ExtractObsWrapper, POMDPWrapper, PPOLearner  # noqa: E402
+from ouzelum_amd.learners.fused import store  # noqa: E402
 from ouzelum_amd.vec_task import make  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -48,14 +49,11 @@ for it in range(a.warmup + a.iters):
     t0 = time.perf_counter()
     init = (lstm[0].clone(), lstm[1].clone()) if lstm is not None else None
     for s in range(T):
-        pomdps[s] = pomdp
-        obs[s] = next_obs
-        dones[s] = next_done
+        store((pomdps[s], obs[s], dones[s]), (pomdp, next_obs, next_done))   # one multi-tensor copy (fused.store)
         # alias=True: the policy graph's output buffers, as learners/train.py's loop takes them (actions[s] /
         # logprobs[s] copy them before the next replay); alias=False adds 5 clones per step
         act, lp, _, lstm = agent.act(next_obs, lstm, next_done, alias=True)
-        actions[s] = act
-        logprobs[s] = lp
+        store((actions[s], logprobs[s]), (act, lp))
         next_obs, rewards[s], next_done, info = env.step(act)
         pomdp = pw.observation(next_obs)
     torch.cuda.synchronize()
