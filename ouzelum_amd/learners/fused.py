@@ -35,8 +35,13 @@ _FUSED_SAMPLE = os.environ.get("OUZ_FUSED_SAMPLE", "1") != "0"
 _SMALLK_TANH = os.environ.get("OUZ_SMALLK_TANH", "1") != "0"
 
 
+_SPLITK = os.environ.get("OUZ_SPLITK", "1") != "0"
+
+
 def _splits(k, n_out_tiles):
-    """Number of K slabs: enough workgroups to cover the chip, slabs of >= 256 rows."""
+    """Number of K slabs: enough workgroups to cover the chip, slabs of >= 256 rows (OUZ_SPLITK=0: one plain GEMM)."""
+    if not _SPLITK:
+        return 1
     for s in (32, 16, 8, 4, 2):
         if k % s == 0 and k // s >= 256 and n_out_tiles * s <= 1024:
             return s
