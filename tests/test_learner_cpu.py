@@ -189,3 +189,15 @@ def test_clip_adam_refuses_cpu_and_unsupported_optimizers():
     obs_s, act_s = Box(-np.inf * np.ones(13), np.inf * np.ones(13)), Box(-np.ones(4), np.ones(4))
     ag = PPOLearner(obs_s, act_s, 8, "cpu", recurrent=False, num_minibatches=1, update_epochs=1)
     assert ag._clip_adam is None
+
+
+def test_store_copies_every_pair():
+    """fused.store (the rollout loop's storage writes; one multi-tensor copy on a GPU) copies each source into its
+    destination slice, here through the per-tensor fallback of CPU tensors."""
+    import torch
+    from ouzelum_amd.learners.fused import store
+    obs, dones = torch.zeros(4, 8, 13), torch.zeros(4, 8)
+    o, d = torch.randn(8, 13), torch.rand(8)
+    store((obs[2], dones[2]), (o, d))
+    assert torch.equal(obs[2], o) and torch.equal(dones[2], d)
+    assert float(obs[[0, 1, 3]].abs().sum()) == 0.0 and float(dones[[0, 1, 3]].abs().sum()) == 0.0
